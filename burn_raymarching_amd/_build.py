@@ -1,0 +1,74 @@
+"""Build recipe for the in-tree native libraries (hipcc for gfx950; no JIT cache).
+
+  burn_raymarching_amd/lib/libraymarch_hip.so  <- csrc/rm_kernels.hip   (the product: C ABI of include/raymarch.h)
+  burn_raymarching_amd/lib/rm_train             <- csrc/host/*.cpp       (C++ host: Scene/Camera/train loop)
+
+Run ``python -m burn_raymarching_amd._build`` or ``__graft_entry__.build()``.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIBDIR = os.path.join(PKG, "lib")
+ARCH = os.environ.get("RM_OFFLOAD_ARCH", "gfx950")
+LIB = os.path.join(LIBDIR, "libraymarch_hip.so")
+
+
+def _hipcc() -> str:
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the HIP toolchain is required to build libraymarch_hip.so")
+
+
+def _stale(target: str, sources) -> bool:
+    if not os.path.exists(target):
+        return True
+    t = os.path.getmtime(target)
+    return any(os.path.getmtime(s) > t for s in sources)
+
+
+def build_lib(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(LIBDIR, exist_ok=True)
+    srcs = [os.path.join(CSRC, "rm_kernels.hip"), os.path.join(CSRC, "rm_device.h"),
+            os.path.join(ROOT, "include", "raymarch.h")]
+    if force or _stale(LIB, srcs):
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+               "-Wall", "-Wno-unused-result", "-o", LIB, srcs[0]]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+    return LIB
+
+
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    """C++ host (train loop) linked against libraymarch_hip.so."""
+    host_dir = os.path.join(CSRC, "host")
+    if not os.path.isdir(host_dir):
+        return ""
+    lib = build_lib(force=force, verbose=verbose)
+    exe = os.path.join(LIBDIR, "rm_train")
+    srcs = sorted(os.path.join(host_dir, f) for f in os.listdir(host_dir) if f.endswith((".cpp", ".hpp")))
+    cpp = [s for s in srcs if s.endswith(".cpp")]
+    if force or _stale(exe, srcs + [lib, os.path.join(ROOT, "include", "raymarch.h")]):
+        cmd = [_hipcc(), "-O2", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"), "-o", exe] + cpp + [
+            "-L", LIBDIR, "-lraymarch_hip", f"-Wl,-rpath,{LIBDIR}", "-Wl,-rpath,$ORIGIN", "-lz"]
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
+    return exe
+
+
+def build_all(force: bool = False, verbose: bool = False) -> None:
+    build_lib(force=force, verbose=verbose)
+    build_host(force=force, verbose=verbose)
+
+
+if __name__ == "__main__":
+    build_all(force="--force" in sys.argv, verbose=True)

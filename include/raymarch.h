@@ -1,0 +1,166 @@
+/*
+ * raymarch.h -- C ABI of libraymarch_hip.so, the MI355X (gfx950) differentiable
+ * SDF-sphere raymarcher.
+ *
+ * This boundary replaces the reference's hot path, the per-ray differentiable
+ * render of kokutoupan/burn_raymarching:
+ *
+ *   render_diff<B: Backend>(ray_org [N,3], ray_dir [N,3], centers [M,3], colors [M,3],
+ *                           radius [M,1], light_dir [3], ambient [1], smooth_k: f32)
+ *       -> Tensor<B,2> [N,3]                              (src/renderer_diff.rs:6-15)
+ *
+ * called from SceneModel::forward (src/model/scene.rs:35-57) by the training step
+ * (src/bin/train.rs:182) and the preview (src/bin/train.rs:355), together with its
+ * gradient, which the reference gets from burn-autodiff via loss.backward()
+ * (src/bin/train.rs:189-190). The reference has no FFI for this path; a Rust host
+ * would bind these entry points with `extern "C"`.
+ *
+ * Conventions
+ *  - Every tensor argument is a caller-owned DEVICE pointer to fp32, row-major, AoS
+ *    [n][3] exactly like the reference's tensors. Camera descriptors are host structs.
+ *  - Scene parameters are the ACTIVATED values render_diff receives
+ *    (scene.rs:41-45): colors = sigmoid(raw), radius = softplus(raw)+0.01,
+ *    ambient = sigmoid(raw), light_dir raw (normalised inside, renderer_diff.rs:49-50).
+ *    rm_scene_activate() produces them from the raw Param tensors.
+ *  - Every call is asynchronous on the context's stream; the caller synchronises.
+ *  - Return value: RM_OK (0) or an RM_ERR_* code; rm_last_error() has the text.
+ *    Invalid arguments never launch work. A context is not thread-safe; use one
+ *    context per host thread / stream.
+ *  - Results are deterministic: every cross-ray sum is reduced in a fixed order.
+ */
+#ifndef RAYMARCH_H_
+#define RAYMARCH_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RM_OK 0
+#define RM_ERR_INVALID_ARG 1
+#define RM_ERR_HIP 2
+#define RM_ERR_OOM 3
+#define RM_ERR_UNSUPPORTED 4
+
+/* Limits of this build. */
+#define RM_MAX_VIEWS_PER_CALL 16     /* camera descriptors per rm_*_camera call */
+#define RM_MAX_SPHERES 65536
+
+typedef struct rm_context rm_context;
+
+/* Activated scene parameters (device pointers), scene.rs:9-16 after scene.rs:41-45. */
+typedef struct rm_scene {
+  const float* centers;   /* [M,3]                                      */
+  const float* colors;    /* [M,3] sigmoid(raw colors)                   */
+  const float* radius;    /* [M]   softplus(raw radius) + 0.01           */
+  const float* light_dir; /* [3]   raw light direction                   */
+  const float* ambient;   /* [1]   sigmoid(raw ambient)                  */
+  int32_t num_spheres;    /* M >= 1                                      */
+} rm_scene;
+
+/* March / shading constants. rm_march_default() fills the reference's values. */
+typedef struct rm_march {
+  int32_t steps;          /* fixed march steps, renderer_diff.rs:22 (40)             */
+  float smooth_k;         /* soft-min sharpness k, sdf.rs:30 (train 5->32, preview 32) */
+  float normal_eps;       /* finite-difference normal step, scene.rs:91 (1e-4)       */
+  float color_sharpness;  /* softmax(-c * dist) colour blend, renderer_diff.rs:74 (10) */
+  float mask_sharpness;   /* sigmoid(-c * D) silhouette, renderer_diff.rs:88 (15)     */
+} rm_march;
+
+/* Pinhole LookAt camera, camera.rs:30-37. Rays are generated in-kernel exactly as
+ * create_camera_rays (camera.rs:41-87): rows y then x, u = x/W*2-1, v = -(y/H*2-1). */
+typedef struct rm_camera {
+  float eye[3];
+  float target[3];
+  float fov_deg;
+} rm_camera;
+
+/* Gradient outputs (device pointers) w.r.t. the ACTIVATED parameters, except
+ * light_dir which is w.r.t. the raw light direction (the normalisation is inside
+ * render_diff). Any pointer may be NULL to skip that output. */
+typedef struct rm_grads {
+  float* centers;    /* [M,3] */
+  float* colors;     /* [M,3] */
+  float* radius;     /* [M]   */
+  float* light_dir;  /* [3]   */
+  float* ambient;    /* [1]   */
+} rm_grads;
+
+/* ---- context --------------------------------------------------------------- */
+const char* rm_version(void);
+/* stream: a hipStream_t (NULL = the null stream). */
+int rm_create(int32_t device, void* stream, rm_context** out_ctx);
+int rm_set_stream(rm_context* ctx, void* stream);
+void rm_destroy(rm_context* ctx);
+const char* rm_last_error(const rm_context* ctx);
+void rm_march_default(rm_march* m);
+/* Pre-size the workspace for backward/train calls of up to max_rays rays and
+ * max_spheres spheres so later calls never allocate (needed for hipGraph capture). */
+int rm_reserve(rm_context* ctx, int64_t max_rays, int32_t max_spheres);
+
+/* ---- forward: renderer_diff.rs:6-91 --------------------------------------- */
+/* out [N,3] receives render_diff(ray_org, ray_dir, scene..., smooth_k).
+ * t_march (nullable) [N] receives the detached march distance t after `steps`
+ * steps (renderer_diff.rs:20-26), which rm_render_diff_backward can reuse. */
+int rm_render_diff(rm_context* ctx, const float* ray_org, const float* ray_dir, int64_t num_rays,
+                   const rm_scene* scene, const rm_march* march, float* out, float* t_march);
+/* Camera mode: rays of `num_views` cameras at width x height generated in-kernel;
+ * out is [num_views*height*width, 3] in view, row, column order. */
+int rm_render_diff_camera(rm_context* ctx, const rm_camera* cams, int32_t num_views, int32_t width,
+                          int32_t height, const rm_scene* scene, const rm_march* march, float* out,
+                          float* t_march);
+
+/* ---- backward: the burn-autodiff gradient of render_diff ------------------ */
+/* grad_out [N,3] = dL/d(out). t_march (nullable) = the forward's saved march t;
+ * when given the march is not replayed. accumulate != 0 adds into the grads. */
+int rm_render_diff_backward(rm_context* ctx, const float* ray_org, const float* ray_dir, int64_t num_rays,
+                            const rm_scene* scene, const rm_march* march, const float* grad_out,
+                            const float* t_march, const rm_grads* grads, int32_t accumulate);
+int rm_render_diff_backward_camera(rm_context* ctx, const rm_camera* cams, int32_t num_views, int32_t width,
+                                   int32_t height, const rm_scene* scene, const rm_march* march,
+                                   const float* grad_out, const float* t_march, const rm_grads* grads,
+                                   int32_t accumulate);
+
+/* ---- fused train step: forward + compute_loss seed + backward ------------- */
+/* The reconstruction term of compute_loss (training.rs:17-34): for each ray,
+ * W = 10 where sum(target) > 0.01 else 1 + 4*progress, loss += sum_c |out-target|*W,
+ * g = W*sign(out-target)*inv_count (inv_count = 1/(3*N_global) gives the mean).
+ * loss_sum (device, 1 float) receives sum |out-target|*W (multiply by inv_count
+ * for the mean), added to its current value when accumulate != 0. out (nullable)
+ * receives the forward image. targets are linear RGB [N,3]. */
+int rm_train_step(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
+                  int64_t num_rays, float progress, float inv_count, const rm_scene* scene,
+                  const rm_march* march, const rm_grads* grads, float* loss_sum, float* out,
+                  int32_t accumulate);
+int rm_train_step_camera(rm_context* ctx, const rm_camera* cams, int32_t num_views, int32_t width,
+                         int32_t height, const float* targets, float progress, float inv_count,
+                         const rm_scene* scene, const rm_march* march, const rm_grads* grads,
+                         float* loss_sum, float* out, int32_t accumulate);
+
+/* ---- model helpers: SceneModel activations, compute_loss penalties, Adam ---- */
+/* Packed parameter layout used by the helpers (raw Param tensors or their grads):
+ *   [centers 3M | colors 3M | radius M | light_dir 3 | ambient 1]  (7M+4 floats)
+ * rm_scene_activate writes the activated values in the same packed layout
+ * (scene.rs:41-45) so an rm_scene can point into it (see rm_scene_from_packed). */
+int rm_scene_activate(rm_context* ctx, const float* raw_packed, int32_t num_spheres, float* act_packed);
+void rm_scene_from_packed(const float* act_packed, int32_t num_spheres, rm_scene* out_scene);
+void rm_grads_from_packed(float* grad_packed, int32_t num_spheres, rm_grads* out_grads);
+
+/* Optimizer step on the raw packed params (train.rs:161-198): the activated-space
+ * gradient (packed, e.g. all-reduced across ranks) is chained through scene.rs:41-45,
+ * the compute_loss parameter penalties (training.rs:38-82) are added when
+ * with_penalties != 0, then Burn's Adam (beta1 0.9, beta2 0.999, eps 1e-5) with
+ * coupled L2 weight decay `weight_decay` updates raw_packed in place. adam_m and
+ * adam_v are (7M+4)-float device buffers (zero them when re-initialising the
+ * optimizer, train.rs:160-163); step counts from 1. loss_penalty (nullable, device
+ * float) receives the penalty value. */
+int rm_optimizer_step(rm_context* ctx, float* raw_packed, const float* grad_act_packed, float* adam_m,
+                      float* adam_v, int32_t num_spheres, int32_t step, float lr, float weight_decay,
+                      int32_t with_penalties, float* loss_penalty);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RAYMARCH_H_ */

@@ -1,0 +1,65 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); parity tests through the C ABI")
+    config.addinivalue_line("markers", "slow: larger cases")
+
+
+@pytest.fixture(scope="session")
+def golden_dir():
+    return GOLDEN
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    from oracle import oracle as orc
+    orc.build()
+    return orc
+
+
+def load_png(path):
+    from PIL import Image
+    return np.asarray(Image.open(path).convert("RGB"))
+
+
+def final1_scene():
+    """scene.json (reference, N=6) with the +0.01 radius offset render_diff saw (scene.rs:43 vs
+    train.rs:216): colours and ambient are stored post-sigmoid, light_dir raw."""
+    sc = json.load(open(os.path.join(GOLDEN, "scene.json")))
+    return {
+        "centers": np.array(sc["centers"], np.float32).reshape(-1, 3),
+        "colors": np.array(sc["colors"], np.float32).reshape(-1, 3),
+        "radius": (np.array(sc["radii"], np.float32) + np.float32(0.01)).astype(np.float32),
+        "light_dir": np.array(sc["light_dir"], np.float32),
+        "ambient": np.array(sc["ambient_intensity"], np.float32),
+    }
+
+
+# train.rs:37-44: the preview camera that produced steps/final_1.png
+FINAL1_CAMERA = ([0.0, 0.0, -2.5], [0.0, 0.0, 0.0], 50.0)
+
+# generate.rs:29-40: the target "dango" scene
+DANGO = {
+    "centers": np.array([[-0.3, 0.0, 0.0], [0.0, 0.0, 0.0], [0.3, 0.0, 0.0]], np.float32),
+    "colors": np.eye(3, dtype=np.float32),
+    "radius": np.array([0.2, 0.15, 0.2], np.float32),
+}
+
+
+def gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False

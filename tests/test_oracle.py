@@ -1,0 +1,143 @@
+"""CPU tests of the oracle itself: pinned by the reference's own fixtures (forward) and by
+torch fp64 autograd of a literal op-by-op restatement (backward)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import DANGO, FINAL1_CAMERA, GOLDEN, final1_scene, load_png
+
+
+def test_final1_png_kat(oracle):
+    """steps/final_1.png <- render_diff(scene.json, radius+0.01), S=40, k=32, 256^2 (train.rs:267-274, :355)."""
+    sc = final1_scene()
+    o, d = oracle.camera_rays(256, 256, *FINAL1_CAMERA)
+    out = oracle.render_diff(o, d, sc, 40, 32.0, precision="f32")
+    png = oracle.to_png_bytes(out).reshape(256, 256, 3).astype(int)
+    ref = load_png(os.path.join(GOLDEN, "final_1.png")).astype(int)
+    diff = np.abs(png - ref)
+    assert diff.max() <= 1, diff.max()
+    assert (diff > 0).sum() <= 16
+
+
+def test_final1_needs_radius_offset(oracle):
+    """Without the +0.01 of scene.rs:43 the fixture is NOT reproduced (guards the fixture's meaning)."""
+    sc = final1_scene()
+    sc["radius"] = (sc["radius"] - np.float32(0.01)).astype(np.float32)
+    o, d = oracle.camera_rays(256, 256, *FINAL1_CAMERA)
+    out = oracle.render_diff(o, d, sc, 40, 32.0, precision="f32")
+    png = oracle.to_png_bytes(out).reshape(256, 256, 3).astype(int)
+    ref = load_png(os.path.join(GOLDEN, "final_1.png")).astype(int)
+    assert np.abs(png - ref).max() > 20
+
+
+@pytest.mark.parametrize("view", range(10))
+def test_target_png_kat(oracle, view):
+    """data/target_i.png <- render (renderer.rs) of the generate.rs scene from data/cameras.json."""
+    cams = json.load(open(os.path.join(GOLDEN, "cameras.json")))
+    c = cams[view]
+    o, d = oracle.camera_rays(256, 256, c["origin"], c["target"], c["fov"])
+    out = oracle.render(o, d, DANGO["centers"], DANGO["colors"], DANGO["radius"])
+    png = oracle.to_png_bytes(out).reshape(256, 256, 3).astype(int)
+    ref = load_png(os.path.join(GOLDEN, "target_%d.png" % view)).astype(int)
+    diff = np.abs(png - ref)
+    assert diff.max() <= 1
+    assert (diff > 0).sum() <= 64
+
+
+def _torch_params(sc):
+    def t(x, shape):
+        return torch.tensor(np.asarray(x, np.float64).reshape(shape), requires_grad=True)
+    return (t(sc["centers"], (-1, 3)), t(sc["colors"], (-1, 3)), t(sc["radius"], (-1, 1)),
+            t(sc["light_dir"], (3,)), t(sc["ambient"], (1,)))
+
+
+@pytest.mark.parametrize("k,steps", [(5.0, 16), (32.0, 16), (32.0, 40)])
+def test_backward_matches_autograd(oracle, k, steps):
+    """Analytic backward (rm_oracle_impl.h) == torch fp64 autograd of renderer_diff.rs restated."""
+    from oracle import autodiff_ref as ad
+    from burn_raymarching_amd.model import synthetic_scene, ring_cameras
+    sc = synthetic_scene(8, seed=3)
+    sc["radius"] = sc["radius"] + 0.04
+    eye, tgt, fov = ring_cameras(6)[2]
+    o, d = oracle.camera_rays(12, 12, eye, tgt, fov, precision="f64")
+    g = np.random.default_rng(7).normal(size=o.shape)
+    c, col, r, ld, a = _torch_params(sc)
+    out = ad.render_diff(torch.tensor(o), torch.tensor(d), c, col, r, ld, a, k, steps=steps)
+    (out * torch.tensor(g)).sum().backward()
+    ref = {"centers": c.grad, "colors": col.grad, "radius": r.grad, "light_dir": ld.grad, "ambient": a.grad}
+    fwd = oracle.render_diff(o, d, sc, steps, k, precision="f64")
+    assert np.abs(out.detach().numpy() - fwd).max() < 1e-10
+    got = oracle.render_diff_backward(o, d, sc, steps, k, g, precision="f64")
+    for key, v in ref.items():
+        v = v.numpy().reshape(-1)
+        rel = np.abs(got[key].reshape(-1) - v).max() / max(np.abs(v).max(), 1e-30)
+        assert rel < 1e-9, (key, rel)
+
+
+def test_train_step_seed_matches_autograd(oracle):
+    """Fused train step == autograd of compute_loss's reconstruction term (training.rs:17-34)."""
+    from oracle import autodiff_ref as ad
+    from burn_raymarching_amd.model import synthetic_scene, ring_cameras
+    sc = synthetic_scene(8, seed=4)
+    eye, tgt, fov = ring_cameras(4)[0]
+    o, d = oracle.camera_rays(10, 10, eye, tgt, fov, precision="f64")
+    rng = np.random.default_rng(0)
+    tg = rng.uniform(0, 0.3, size=o.shape)
+    tg[::3] = 0.0  # background pixels (sum <= 0.01)
+    progress = 0.37
+    c, col, r, ld, a = _torch_params(sc)
+    out = ad.render_diff(torch.tensor(o), torch.tensor(d), c, col, r, ld, a, 20.0, steps=12)
+    tt = torch.tensor(tg)
+    w = torch.where(tt.sum(1, keepdim=True) > 0.01, torch.full_like(tt, 10.0), torch.full_like(tt, 1 + 4 * progress))
+    loss = ((out - tt).abs() * w).mean()
+    loss.backward()
+    o_out, loss_sum, got = oracle.train_step(o, d, tg, sc, 12, 20.0, progress)
+    assert abs(loss_sum / (3 * o.shape[0]) - loss.item()) < 1e-12
+    for key, v in {"centers": c.grad, "colors": col.grad, "radius": r.grad, "light_dir": ld.grad,
+                   "ambient": a.grad}.items():
+        v = v.numpy().reshape(-1)
+        rel = np.abs(got[key].reshape(-1) - v).max() / max(np.abs(v).max(), 1e-30)
+        assert rel < 1e-9, (key, rel)
+
+
+def test_fp32_order_within_budget(oracle):
+    """The fp32 reference-order restatement stays inside the stated tolerance of the fp64 anchor."""
+    from burn_raymarching_amd.model import synthetic_scene, ring_cameras
+    sc = synthetic_scene(64, seed=0)
+    eye, tgt, fov = ring_cameras(4)[1]
+    o64, d64 = oracle.camera_rays(48, 48, eye, tgt, fov, precision="f64")
+    o32, d32 = oracle.camera_rays(48, 48, eye, tgt, fov, precision="f32")
+    a = oracle.render_diff(o64, d64, sc, 32, 32.0, precision="f64")
+    b = oracle.render_diff(o32, d32, sc, 32, 32.0, precision="f32")
+    e = np.abs(a - b)
+    assert e.max() < 1e-3 and e.mean() < 1e-5
+
+
+def test_camera_rays_match_reference_formula(oracle):
+    """camera.rs:58-78 corner pixel: u=-1, v=+1 (no half-pixel offset)."""
+    o, d = oracle.camera_rays(4, 2, [0, 0, -2.5], [0, 0, 0], 90.0, precision="f64")
+    assert np.allclose(o, [[0, 0, -2.5]] * 8)
+    # 90 deg fov -> half_h = 1, aspect 2 -> half_w = 2; pixel (0,0): (-2, 1, 1)/|.| in (right, up, fwd)
+    # LookAt along +z: right = fwd x up = (0,0,1)x(0,1,0) = (-1,0,0)
+    v = np.array([2.0, 1.0, 1.0])
+    assert np.allclose(d[0], v / np.linalg.norm(v), atol=1e-7)
+
+
+def test_penalty_and_adam_reference_formulas():
+    """compute_loss penalties (training.rs:38-82) restated in oracle/autodiff_ref.py are
+    differentiable and finite (their GPU twin is checked in test_gpu_parity.py)."""
+    from oracle import autodiff_ref as ad
+    rng = np.random.default_rng(0)
+    m = 6
+    raw = {"centers": torch.tensor(rng.normal(scale=0.5, size=(m, 3)), requires_grad=True),
+           "colors": torch.tensor(rng.normal(size=(m, 3)), requires_grad=True),
+           "radius": torch.tensor(rng.normal(size=(m, 1)), requires_grad=True),
+           "light_dir": torch.tensor([0.0, 1.0, 0.0], dtype=torch.float64, requires_grad=True),
+           "ambient": torch.tensor([-1.4], dtype=torch.float64, requires_grad=True)}
+    out = torch.zeros((4, 3), dtype=torch.float64)
+    loss = ad.compute_loss(raw, out, torch.zeros_like(out), 0.5)
+    loss.backward()
+    assert torch.isfinite(raw["centers"].grad).all()
