@@ -16,7 +16,7 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kSphereAlign = 32;         // M is padded to a multiple of this
 constexpr int kChunkBwd = 32;            // spheres per backward partial-combine chunk
 constexpr float kLog2e = 1.4426950408889634f;
-constexpr float kPadCenterSq = 1e30f;    // padding sphere: |c|^2 huge -> exp() underflows to 0
+constexpr float kPadCenter = 1e15f;      // padding sphere center x: distance ~1e15 -> exp() underflows to 0
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 __device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }
@@ -77,19 +77,25 @@ struct CamBasis {
   float half_w, half_h;
 };
 
-// camera.rs:58-78 for pixel (x, y): precise division/sqrt like the reference's f32 loop.
+// camera.rs:58-78 for pixel (x, y), bit-identical to the reference's f32 loop:
+//  * no FMA contraction (hipcc contracts by default and __fmul_rn/__fadd_rn are plain * and +,
+//    so only the pragma stops it);
+//  * f32 division is correctly rounded on gfx950, but sqrtf/__fsqrt_rn lower to v_sqrt_f32,
+//    which is not (measured: 14.9% of inputs in [1,4) off by 1 ulp); the f64 sqrt rounded to
+//    f32 is exact. Once per ray: free.
 __device__ __forceinline__ void camera_ray(const CamBasis& c, int x, int y, int W, int H, float o[3],
                                            float d[3]) {
+#pragma clang fp contract(off)
   const float u = ((float)x / (float)W) * 2.0f - 1.0f;
   const float v = -(((float)y / (float)H) * 2.0f - 1.0f);
   const float rs = u * c.half_w, us = v * c.half_h;
-  float dx = __fadd_rn(__fadd_rn(__fmul_rn(c.right[0], rs), __fmul_rn(c.up[0], us)), c.fwd[0]);
-  float dy = __fadd_rn(__fadd_rn(__fmul_rn(c.right[1], rs), __fmul_rn(c.up[1], us)), c.fwd[1]);
-  float dz = __fadd_rn(__fadd_rn(__fmul_rn(c.right[2], rs), __fmul_rn(c.up[2], us)), c.fwd[2]);
-  const float len = __fsqrt_rn(__fadd_rn(__fadd_rn(__fmul_rn(dx, dx), __fmul_rn(dy, dy)), __fmul_rn(dz, dz)));
-  d[0] = __fdiv_rn(dx, len);
-  d[1] = __fdiv_rn(dy, len);
-  d[2] = __fdiv_rn(dz, len);
+  const float dx = c.right[0] * rs + c.up[0] * us + c.fwd[0];
+  const float dy = c.right[1] * rs + c.up[1] * us + c.fwd[1];
+  const float dz = c.right[2] * rs + c.up[2] * us + c.fwd[2];
+  const float len = (float)__builtin_sqrt((double)(dx * dx + dy * dy + dz * dz));
+  d[0] = dx / len;
+  d[1] = dy / len;
+  d[2] = dz / len;
   o[0] = c.eye[0];
   o[1] = c.eye[1];
   o[2] = c.eye[2];

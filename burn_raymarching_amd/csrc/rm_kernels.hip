@@ -65,6 +65,7 @@ struct KArgs {
   const float* gout;
   const float* targets;
   float progress, inv_count;
+  float* dbg;       // optional per-ray intermediates [n][16] (diagnostics; see rm_debug_intermediates)
   float* partials;  // [gridDim.x][rec], rec = Mpad*12 + 8
   long long rec;
 };
@@ -86,8 +87,11 @@ __device__ __forceinline__ void stage_tile(const KArgs& a, const Lds& L, int t0,
       L.geo[jl] = make_float4(-2.0f * cx, -2.0f * cy, -2.0f * cz, cx * cx + cy * cy + cz * cz);
       L.col[jl] = make_float4(a.colors[3 * j], a.colors[3 * j + 1], a.colors[3 * j + 2], 0.0f);
       L.krr[jl] = make_float2(kappa * r, r);
-    } else {  // padding sphere: exp() of its soft-min / softmax terms underflows to exactly 0
-      L.geo[jl] = make_float4(0.0f, 0.0f, 0.0f, kPadCenterSq);
+    } else {
+      // padding sphere at c = (kPadCenter, 0, 0): both the expansion form (|c|^2 term) and the
+      // direct form of the normal taps (p - c) see distance ~1e15, so every exp() of its
+      // soft-min / softmax terms underflows to exactly 0 and its gradient terms are exactly 0.
+      L.geo[jl] = make_float4(-2.0f * kPadCenter, 0.0f, 0.0f, kPadCenter * kPadCenter);
       L.col[jl] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
       L.krr[jl] = make_float2(0.0f, 0.0f);
     }
@@ -184,11 +188,13 @@ __device__ __forceinline__ void shade_sweep(float px, float py, float pz, float 
     C[2] *= sw;
     Zb *= sb;
     dmin = dn;
-    const float bw = dn * c10l, bb = dn * kappa;
 #pragma unroll
     for (int jj = 0; jj < 8; ++jj) {
-      const float ew = fexp2(fmaf(dl[jj], -c10l, bw));
-      const float eb = fexp2(fmaf(dl[jj], -kappa, bb));
+      // (dn - dl) <= 0 exactly: dn is the minimum of these very values, so the exponents can
+      // never overflow however large |p| gets (miss rays march to |p| ~ 1e9 and beyond).
+      const float dd = dn - dl[jj];
+      const float ew = fexp2(dd * c10l);
+      const float eb = fexp2(dd * kappa);
       const float4 c = L.col[j0 + jj];
       Zw += ew;
       C[0] = fmaf(ew, c.x, C[0]);
@@ -280,6 +286,7 @@ __global__ __launch_bounds__(kBlock) void rm_ray_kernel(const KArgs a) {
 
   // ---- detached 6-tap normal (scene.rs:81-128)
   float nrm[3];
+  float D6[6];
   {
     float m6[6], s6[6];
 #pragma unroll
@@ -289,7 +296,6 @@ __global__ __launch_bounds__(kBlock) void rm_ray_kernel(const KArgs a) {
     }
     const float eps = a.eps;
     for_tiles([&](int, int tn) { lse_taps(p, L, tn, nkappa, 2.0f * eps, eps * eps, m6, s6); });
-    float D6[6];
 #pragma unroll
     for (int q = 0; q < 6; ++q) D6[q] = -(flog2(fmaxf(s6[q], 1e-8f)) + m6[q]) * inv_kappa;
     const float nx = D6[0] - D6[1], ny = D6[2] - D6[3], nz = D6[4] - D6[5];
@@ -320,6 +326,13 @@ __global__ __launch_bounds__(kBlock) void rm_ray_kernel(const KArgs a) {
   const float scale = Lgt * mu;
   const float outv[3] = {mix[0] * scale, mix[1] * scale, mix[2] * scale};
 
+  if (MODE == kFwd && a.dbg != nullptr && valid) {
+    float* q = a.dbg + 24 * ri;
+    const float vals[24] = {t, tf, nrm[0], nrm[1], nrm[2], Lgt, mix[0], mix[1], mix[2], Df, mu, sdot, dmin,
+                            Zw, Zb, 0.0f, D6[0], D6[1], D6[2], D6[3], D6[4], D6[5], 0.0f, 0.0f};
+#pragma unroll
+    for (int c = 0; c < 24; ++c) q[c] = vals[c];
+  }
   const bool write_out = (MODE == kFwd || MODE == kTrain) && a.out != nullptr && valid;
   if (write_out) {
     a.out[3 * ri] = outv[0];
@@ -359,7 +372,6 @@ __global__ __launch_bounds__(kBlock) void rm_ray_kernel(const KArgs a) {
   const float gell[3] = {gs * nrm[0], gs * nrm[1], gs * nrm[2]};
   const float cmu = gmu * mu * (1.0f - mu) * (-a.msharp);
   const float mg = fmaf(mix[2], gm[2], fmaf(mix[1], gm[1], mix[0] * gm[0]));
-  const float bw = dmin * c10l, bb = dmin * kappa;
   const float b_scale = cmu * frcp(Zb);
   const float ncs = -a.csharp;
 
@@ -378,11 +390,12 @@ __global__ __launch_bounds__(kBlock) void rm_ray_kernel(const KArgs a) {
         const float2 kr = L.krr[j];
         const float4 c4 = L.col[j];
         const float q = qexp(p[0], p[1], p[2], pp, gg);
-        const float qc = fmaxf(q, 1e-6f);
-        const float ir = frsq(qc);
-        const float dl = qc * ir - kr.y;
-        const float w = fexp2(fmaf(dl, -c10l, bw)) * invZw;
-        const float bt = fexp2(fmaf(dl, -kappa, bb)) * b_scale;
+        const float rho = fsqrt(fmaxf(q, 1e-6f));  // bitwise the forward's value (shade_sweep)
+        const float dl = rho - kr.y;
+        const float ir = frcp(rho);
+        const float dd = dmin - dl;                 // <= 0 exactly
+        const float w = fexp2(dd * c10l) * invZw;
+        const float bt = fexp2(dd * kappa) * b_scale;
         const float cg = fmaf(c4.z, gm[2], fmaf(c4.y, gm[1], c4.x * gm[0]));
         const float gd = fmaf(w * ncs, cg - mg, bt);
         const float gu = q >= 1e-6f ? gd * ir : 0.0f;  // clamp_min(1e-6) gate
@@ -421,9 +434,9 @@ __global__ __launch_bounds__(kBlock) void rm_ray_kernel(const KArgs a) {
           const float4 gg = L.geo[j];
           const float kr = L.krr[j].x;
           const float q = qexp(pa[0], pa[1], pa[2], ppa, gg);
-          const float qc = fmaxf(q, 1e-6f);
-          const float ir = frsq(qc);
-          const float h = fexp2(fmaf(qc * ir, nkappa, kr) - mA) * hsc;
+          const float rho = fsqrt(fmaxf(q, 1e-6f));  // bitwise the reconnect sweep's value
+          const float ir = frcp(rho);
+          const float h = fexp2(fmaf(rho, nkappa, kr) - mA) * hsc;  // v - mA <= 0 exactly
           const float hu = q >= 1e-6f ? h * ir : 0.0f;
           vals[4 * u + 0] = -hu * fmaf(0.5f, gg.x, pa[0]);
           vals[4 * u + 1] = -hu * fmaf(0.5f, gg.y, pa[1]);
@@ -787,6 +800,7 @@ struct Call {
   const float* gout = nullptr;
   const float* targets = nullptr;
   float progress = 0.0f, inv_count = 0.0f;
+  float* dbg = nullptr;
   const rm_grads* grads = nullptr;
   float* loss_sum = nullptr;
   int accumulate = 0;
@@ -823,7 +837,7 @@ int run(rm_context* ctx, const Call& c) {
     if (c.n > 0 && (!c.org || !c.dir)) return fail(ctx, RM_ERR_INVALID_ARG, "ray_org/ray_dir is NULL");
   }
   const long long n = c.cam ? (long long)c.views * c.W * c.H : c.n;
-  if (c.mode == kFwd && !c.out && !c.t_out) return fail(ctx, RM_ERR_INVALID_ARG, "no output requested");
+  if (c.mode == kFwd && n > 0 && !c.out && !c.t_out && !c.dbg) return fail(ctx, RM_ERR_INVALID_ARG, "no output requested");
   if (c.mode == kBwd && n > 0 && !c.gout) return fail(ctx, RM_ERR_INVALID_ARG, "grad_out is NULL");
   if (c.mode == kTrain && n > 0 && !c.targets) return fail(ctx, RM_ERR_INVALID_ARG, "targets is NULL");
   if (c.mode != kFwd && !c.grads) return fail(ctx, RM_ERR_INVALID_ARG, "grads is NULL");
@@ -853,6 +867,7 @@ int run(rm_context* ctx, const Call& c) {
   a.targets = c.targets;
   a.progress = c.progress;
   a.inv_count = c.inv_count;
+  a.dbg = c.dbg;
   a.rec = rec_floats(Mpad);
   const size_t lds = (size_t)tile * (16 + 16 + 8) + (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float);
 
@@ -1069,6 +1084,21 @@ int rm_train_step_camera(rm_context* ctx, const rm_camera* cams, int32_t num_vie
   c.loss_sum = loss_sum;
   c.out = out;
   c.accumulate = accumulate;
+  return run(ctx, c);
+}
+
+int rm_debug_intermediates(rm_context* ctx, const float* ray_org, const float* ray_dir, int64_t num_rays,
+                           const rm_scene* scene, const rm_march* march, float* dbg) {
+  if (!dbg) return fail(ctx, RM_ERR_INVALID_ARG, "dbg is NULL");
+  Call c;
+  c.mode = kFwd;
+  c.cam = false;
+  c.org = ray_org;
+  c.dir = ray_dir;
+  c.n = num_rays;
+  c.scene = scene;
+  c.march = march;
+  c.dbg = dbg;
   return run(ctx, c);
 }
 

@@ -63,6 +63,8 @@ SIGNATURES = {
     "rm_train_step_camera": (ctypes.c_int, [_P, ctypes.POINTER(RmCamera), _I32, _I32, _I32, _P, _F, _F,
                                             ctypes.POINTER(RmScene), ctypes.POINTER(RmMarch),
                                             ctypes.POINTER(RmGrads), _P, _P, _I32]),
+    "rm_debug_intermediates": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.POINTER(RmScene),
+                                              ctypes.POINTER(RmMarch), _P]),
     "rm_scene_activate": (ctypes.c_int, [_P, _P, _I32, _P]),
     "rm_scene_from_packed": (None, [_P, _I32, ctypes.POINTER(RmScene)]),
     "rm_grads_from_packed": (None, [_P, _I32, ctypes.POINTER(RmGrads)]),

@@ -138,6 +138,14 @@ int rm_train_step_camera(rm_context* ctx, const rm_camera* cams, int32_t num_vie
                          const rm_scene* scene, const rm_march* march, const rm_grads* grads,
                          float* loss_sum, float* out, int32_t accumulate);
 
+/* ---- diagnostics ------------------------------------------------------------ */
+/* Per-ray forward intermediates dbg [N][24] = {t, t_final, n.x, n.y, n.z, lighting,
+ * mix.r, mix.g, mix.b, D_final, mask, n.l, min delta, Zw, Zb, 0, D(+x), D(-x), D(+y),
+ * D(-y), D(+z), D(-z), 0, 0} (renderer_diff.rs
+ * stages) for parity debugging against the oracle. Not on the hot path. */
+int rm_debug_intermediates(rm_context* ctx, const float* ray_org, const float* ray_dir, int64_t num_rays,
+                           const rm_scene* scene, const rm_march* march, float* dbg);
+
 /* ---- model helpers: SceneModel activations, compute_loss penalties, Adam ---- */
 /* Packed parameter layout used by the helpers (raw Param tensors or their grads):
  *   [centers 3M | colors 3M | radius M | light_dir 3 | ambient 1]  (7M+4 floats)

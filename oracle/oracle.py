@@ -46,6 +46,8 @@ def lib():
             getattr(_lib, f"orc_train_step_{suf}").argtypes = [
                 ctypes.c_long, _P, _P, _P, real, real, _P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int,
                 real, _P, _P, _P, _P, _P, _P, _P]
+            getattr(_lib, f"orc_render_diff_debug_{suf}").argtypes = [
+                ctypes.c_long, _P, _P, _P, _P, _P, _P, _P, ctypes.c_int, ctypes.c_int, real, _P]
             getattr(_lib, f"orc_render_{suf}").argtypes = [
                 ctypes.c_long, _P, _P, _P, _P, _P, ctypes.c_int, _P]
     return _lib
@@ -102,6 +104,20 @@ def render_diff(ray_org, ray_dir, scene, steps, smooth_k, precision="f64", with_
                                                    _ptr(a), c.shape[0], steps, float(smooth_k), _ptr(out),
                                                    _ptr(t))
     return (out, t) if with_t else out
+
+
+def render_diff_debug(ray_org, ray_dir, scene, steps, smooth_k, precision="f64"):
+    """Per-ray intermediates [N,24] (layout of rm_debug_intermediates)."""
+    dt = _dt(precision)
+    o = _arr(ray_org, dt)
+    d = _arr(ray_dir, dt)
+    c, col, r, ld, a = _scene(scene, dt)
+    n = o.shape[0]
+    dbg = np.zeros((n, 24), dt)
+    getattr(lib(), f"orc_render_diff_debug_{precision}")(n, _ptr(o), _ptr(d), _ptr(c), _ptr(col), _ptr(r),
+                                                         _ptr(ld), _ptr(a), c.shape[0], steps, float(smooth_k),
+                                                         _ptr(dbg))
+    return dbg
 
 
 def _grads(m, dt):

@@ -128,6 +128,7 @@ typedef struct {
   REAL tf;         /* t_final = t + dist_last (renderer_diff.rs:36) */
   REAL p[3];       /* p_final (renderer_diff.rs:39) */
   REAL n[3];       /* detached normal (renderer_diff.rs:41-46) */
+  REAL dd[6];      /* the six tap distances (scene.rs:111) */
   REAL ldn[3], ldlen;
   REAL sdot, diff, L;
   REAL wmax, wsum;  /* colour softmax normalizer over -10*delta (renderer_diff.rs:74) */
@@ -166,6 +167,7 @@ static void FN(forward_ray)(const REAL o[3], const REAL d[3], const REAL* center
       dd[2 * a + sgn] = FN(scene_sdf)(tap, centers, radius, M, k, NULL, NULL);
     }
   }
+  for (int q = 0; q < 6; ++q) f->dd[q] = dd[q];
   REAL nx = dd[0] - dd[1], ny = dd[2] - dd[3], nz = dd[4] - dd[5]; /* scene.rs:119-121 */
   REAL len = SQRT(nx * nx + ny * ny + nz * nz + RF(1e-6));    /* scene.rs:125 */
   f->n[0] = nx / len;
@@ -313,6 +315,24 @@ void FN(orc_render_diff)(long n, const REAL* org, const REAL* dir, const REAL* c
     FN(forward_ray)(org + 3 * i, dir + 3 * i, centers, colors, radius, ld, amb[0], M, steps, k, NULL, &f);
     for (int c = 0; c < 3; ++c) out[3 * i + c] = f.out[c];
     if (t_march) t_march[i] = f.t;
+  }
+}
+
+/* Diagnostics twin of rm_debug_intermediates: dbg [N][24] = {t, t_final, n, lighting, mix,
+ * D_final, mask, n.l, min delta, Zw (shifted at min delta), Zb (shifted), 0}. */
+void FN(orc_render_diff_debug)(long n, const REAL* org, const REAL* dir, const REAL* centers, const REAL* colors,
+                               const REAL* radius, const REAL* ld, const REAL* amb, int M, int steps, REAL k,
+                               REAL* dbg) {
+#pragma omp parallel for schedule(dynamic, 64)
+  for (long i = 0; i < n; ++i) {
+    FN(RayFwd) f;
+    FN(forward_ray)(org + 3 * i, dir + 3 * i, centers, colors, radius, ld, amb[0], M, steps, k, NULL, &f);
+    REAL* q = dbg + 24 * i;
+    q[0] = f.t; q[1] = f.tf; q[2] = f.n[0]; q[3] = f.n[1]; q[4] = f.n[2]; q[5] = f.L;
+    q[6] = f.mix[0]; q[7] = f.mix[1]; q[8] = f.mix[2]; q[9] = f.Df; q[10] = f.mu; q[11] = f.sdot;
+    q[12] = f.wmax / RF(-10); q[13] = f.wsum; q[14] = f.bsum; q[15] = RF(0);
+    for (int t = 0; t < 6; ++t) q[16 + t] = f.dd[t];
+    q[22] = q[23] = RF(0);
   }
 }
 
