@@ -16,7 +16,10 @@ constexpr int kWaves = kBlock / 64;
 constexpr int kSphereAlign = 32;         // M is padded to a multiple of this
 constexpr int kChunkBwd = 32;            // spheres per backward partial-combine chunk
 constexpr float kLog2e = 1.4426950408889634f;
+constexpr float kSafeRho = 4e-3f;        // rho >= this => max(q, 1e-6) is a no-op (q >= 1.6e-5)
 constexpr float kPadCenter = 1e15f;      // padding sphere center x: distance ~1e15 -> exp() underflows to 0
+
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 __device__ __forceinline__ float flog2(float x) { return __builtin_amdgcn_logf(x); }

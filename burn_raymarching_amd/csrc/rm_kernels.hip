@@ -28,6 +28,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "../../include/raymarch.h"
 #include "rm_device.h"
@@ -70,136 +73,201 @@ struct KArgs {
   long long rec;
 };
 
-// ---- LDS staging --------------------------------------------------------------------
+// ---- LDS staging: pair-interleaved sphere records ---------------------------------------
+// Pair i holds spheres (2i, 2i+1) so that every sweep runs two spheres per v_pk_* instruction:
+//   P0 = {-2cx0, -2cx1, -2cy0, -2cy1}   P1 = {-2cz0, -2cz1, |c0|^2, |c1|^2}
+//   P2 = {kappa r0, kappa r1, r0, r1}    P3 = {red0, red1, green0, green1}   P4 = {blue0, blue1}
+// (36 B per sphere). All lanes of a wave read the same record: LDS broadcast.
 struct Lds {
-  float4* geo;  // {-2cx, -2cy, -2cz, |c|^2}
-  float4* col;  // {r, g, b, 0}
-  float2* krr;  // {kappa * r, r}
-  float* slots; // backward wave partials, 2 buffers
+  float4* P0;
+  float4* P1;
+  float4* P2;
+  float4* P3;
+  float2* P4;
+  float* slots;  // backward wave partials, 2 buffers
+  float* misc;   // [kWaves] per-wave minimum radius
 };
 
-__device__ __forceinline__ void stage_tile(const KArgs& a, const Lds& L, int t0, int tn, float kappa) {
-  for (int jl = threadIdx.x; jl < tn; jl += kBlock) {
-    const int j = t0 + jl;
-    if (j < a.M) {
-      const float cx = a.centers[3 * j], cy = a.centers[3 * j + 1], cz = a.centers[3 * j + 2];
-      const float r = a.radius[j];
-      L.geo[jl] = make_float4(-2.0f * cx, -2.0f * cy, -2.0f * cz, cx * cx + cy * cy + cz * cz);
-      L.col[jl] = make_float4(a.colors[3 * j], a.colors[3 * j + 1], a.colors[3 * j + 2], 0.0f);
-      L.krr[jl] = make_float2(kappa * r, r);
-    } else {
-      // padding sphere at c = (kPadCenter, 0, 0): both the expansion form (|c|^2 term) and the
-      // direct form of the normal taps (p - c) see distance ~1e15, so every exp() of its
-      // soft-min / softmax terms underflows to exactly 0 and its gradient terms are exactly 0.
-      L.geo[jl] = make_float4(-2.0f * kPadCenter, 0.0f, 0.0f, kPadCenter * kPadCenter);
-      L.col[jl] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-      L.krr[jl] = make_float2(0.0f, 0.0f);
-    }
-  }
+__host__ __device__ constexpr size_t lds_bytes(int tile) {
+  return (size_t)tile * 36 + (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float) + 64;
 }
+
+// Stages spheres [t0, t0 + tn) (tn even); returns this thread's minimum real radius.
+__device__ __forceinline__ float stage_tile(const KArgs& a, const Lds& L, int t0, int tn, float kappa) {
+  float rmin = INFINITY;
+  for (int ip = threadIdx.x; ip < tn / 2; ip += kBlock) {
+    float gx[2], gy[2], gz[2], cc[2], kr[2], rr[2], cr[2], cg[2], cb[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = t0 + 2 * ip + h;
+      if (j < a.M) {
+        const float cx = a.centers[3 * j], cy = a.centers[3 * j + 1], cz = a.centers[3 * j + 2];
+        const float r = a.radius[j];
+        gx[h] = -2.0f * cx;
+        gy[h] = -2.0f * cy;
+        gz[h] = -2.0f * cz;
+        cc[h] = cx * cx + cy * cy + cz * cz;
+        kr[h] = kappa * r;
+        rr[h] = r;
+        cr[h] = a.colors[3 * j];
+        cg[h] = a.colors[3 * j + 1];
+        cb[h] = a.colors[3 * j + 2];
+        rmin = fminf(rmin, r);
+      } else {
+        // padding sphere at c = (kPadCenter, 0, 0): the expansion form (|c|^2) and the direct
+        // form of the normal taps (p - c) both see distance ~1e15, so every exp() of its terms
+        // underflows to exactly 0 and all of its gradient terms are exactly 0.
+        gx[h] = -2.0f * kPadCenter;
+        gy[h] = gz[h] = 0.0f;
+        cc[h] = kPadCenter * kPadCenter;
+        kr[h] = rr[h] = cr[h] = cg[h] = cb[h] = 0.0f;
+      }
+    }
+    L.P0[ip] = make_float4(gx[0], gx[1], gy[0], gy[1]);
+    L.P1[ip] = make_float4(gz[0], gz[1], cc[0], cc[1]);
+    L.P2[ip] = make_float4(kr[0], kr[1], rr[0], rr[1]);
+    L.P3[ip] = make_float4(cr[0], cr[1], cg[0], cg[1]);
+    L.P4[ip] = make_float2(cb[0], cb[1]);
+  }
+  return rmin;
+}
+
+// ---- packed helpers --------------------------------------------------------------------------
+__device__ __forceinline__ f2 sp(float x) { return f2{x, x}; }
+__device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2 sqrt2(f2 q) { return f2{fsqrt(q.x), fsqrt(q.y)}; }
+__device__ __forceinline__ f2 exp2v(f2 x) { return f2{fexp2(x.x), fexp2(x.y)}; }
+__device__ __forceinline__ f2 rcp2(f2 x) { return f2{frcp(x.x), frcp(x.y)}; }
+__device__ __forceinline__ f2 clamp_q(f2 q) { return f2{fmaxf(q.x, 1e-6f), fmaxf(q.y, 1e-6f)}; }
+__device__ __forceinline__ f2 lo(const float4& v) { return f2{v.x, v.y}; }
+__device__ __forceinline__ f2 hi(const float4& v) { return f2{v.z, v.w}; }
+
+// q = |p|^2 + |c|^2 - 2 p.c for a sphere pair (expansion form, scene.rs:66-71). Every sweep that
+// must reproduce another sweep's distances bit for bit uses this one expression.
+__device__ __forceinline__ f2 qpair(const f2& PX, const f2& PY, const f2& PZ, const f2& PP, const float4& A,
+                                    const float4& B) {
+  return fma2(PZ, lo(B), fma2(PY, hi(A), fma2(PX, lo(A), PP + hi(B))));
+}
+__device__ __forceinline__ float psq(const float p[3]) { return fmaf(p[2], p[2], fmaf(p[1], p[1], p[0] * p[0])); }
 
 // ---- forward sweeps -----------------------------------------------------------------
-// q = |p|^2 + |c|^2 - 2 p.c (expansion form, scene.rs:66-71) from the staged record.
-__device__ __forceinline__ float qexp(float px, float py, float pz, float pp, const float4& g) {
-  return fmaf(pz, g.z, fmaf(py, g.y, fmaf(px, g.x, pp + g.w)));
-}
-
-// Base-2 log-sum-exp of v_j = kappa*(r_j - rho_j) over a tile (sdf.rs:36-40), running
-// max m and shifted sum s carried across tiles. Chunks of 16: one rescale exp per chunk.
-__device__ __forceinline__ void lse_point(float px, float py, float pz, float pp, const Lds& L, int n,
-                                          float nkappa, float& m, float& s) {
-  for (int j0 = 0; j0 < n; j0 += 16) {
-    float v[16];
+// Base-2 log-sum-exp of v_j = kappa*(r_j - rho_j) over a tile (sdf.rs:36-40), running max m and
+// shifted sum s carried across tiles; chunks of 16 spheres, one rescale exp per chunk.
+// CLAMP=false drops max(q, 1e-6): only used when the caller proved every rho_j >= kSafeRho.
+template <bool CLAMP>
+__device__ __forceinline__ void lse_point(const float p[3], const Lds& L, int npairs, float nkappa, float& m,
+                                          float& s) {
+  const f2 PX = sp(p[0]), PY = sp(p[1]), PZ = sp(p[2]), PP = sp(psq(p)), NK = sp(nkappa);
+  for (int i0 = 0; i0 < npairs; i0 += 8) {
+    f2 v[8];
 #pragma unroll
-    for (int jj = 0; jj < 16; ++jj) {
-      const float4 g = L.geo[j0 + jj];
-      const float kr = L.krr[j0 + jj].x;
-      v[jj] = fmaf(fsqrt(fmaxf(qexp(px, py, pz, pp, g), 1e-6f)), nkappa, kr);
+    for (int ii = 0; ii < 8; ++ii) {
+      const float4 A = L.P0[i0 + ii], B = L.P1[i0 + ii];
+      const float2 K = reinterpret_cast<const float2*>(L.P2)[2 * (i0 + ii)];
+      f2 q = qpair(PX, PY, PZ, PP, A, B);
+      if constexpr (CLAMP) q = clamp_q(q);
+      v[ii] = fma2(sqrt2(q), NK, f2{K.x, K.y});
     }
-    float cm = v[0];
+    float cm = fmaxf(v[0].x, v[0].y);
 #pragma unroll
-    for (int jj = 1; jj < 16; ++jj) cm = fmaxf(cm, v[jj]);
+    for (int ii = 1; ii < 8; ++ii) cm = fmaxf(cm, fmaxf(v[ii].x, v[ii].y));
     const float mn = fmaxf(m, cm);
-    float s0 = s * fexp2(m - mn), s1 = 0.0f;
+    const f2 MN = sp(mn);
+    f2 acc = f2{s * fexp2(m - mn), 0.0f};
 #pragma unroll
-    for (int jj = 0; jj < 16; jj += 2) {
-      s0 += fexp2(v[jj] - mn);
-      s1 += fexp2(v[jj + 1] - mn);
-    }
-    s = s0 + s1;
+    for (int ii = 0; ii < 8; ++ii) acc += exp2v(v[ii] - MN);
+    s = acc.x + acc.y;
     m = mn;
   }
 }
 
-// The six normal taps p +- eps*e_a (scene.rs:93-111) in one pass over the spheres.
-// q at a tap is formed from e = p - c in direct form, |e +- eps e_a|^2 = |e|^2 + eps^2 +- 2 eps e_a,
-// which keeps the fp32 error of the finite difference ~30x below the expansion form.
-__device__ __forceinline__ void lse_taps(const float p[3], const Lds& L, int n, float nkappa, float two_eps,
+// The six normal taps p +- eps*e_a (scene.rs:93-111) in one pass over the spheres. q at a tap
+// is formed from e = p - c in direct form, |e +- eps e_a|^2 = |e|^2 + eps^2 +- 2 eps e_a, which
+// keeps the fp32 error of the finite difference ~10x below the reference's expansion form.
+template <bool CLAMP>
+__device__ __forceinline__ void lse_taps(const float p[3], const Lds& L, int npairs, float nkappa, float two_eps,
                                          float eps2, float (&m)[6], float (&s)[6]) {
-  for (int j0 = 0; j0 < n; j0 += 8) {
-    float v[6][8];
+  const f2 PX = sp(p[0]), PY = sp(p[1]), PZ = sp(p[2]), NK = sp(nkappa), HALF = sp(0.5f), E2 = sp(eps2),
+           TE = sp(two_eps), NTE = sp(-two_eps);
+  for (int i0 = 0; i0 < npairs; i0 += 4) {
+    f2 v[6][4];
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const float4 g = L.geo[j0 + jj];
-      const float kr = L.krr[j0 + jj].x;
-      const float ex = fmaf(0.5f, g.x, p[0]), ey = fmaf(0.5f, g.y, p[1]), ez = fmaf(0.5f, g.z, p[2]);
-      const float Q = fmaf(ez, ez, fmaf(ey, ey, fmaf(ex, ex, eps2)));
-      const float q[6] = {fmaf(ex, two_eps, Q), fmaf(ex, -two_eps, Q), fmaf(ey, two_eps, Q),
-                          fmaf(ey, -two_eps, Q), fmaf(ez, two_eps, Q), fmaf(ez, -two_eps, Q)};
+    for (int ii = 0; ii < 4; ++ii) {
+      const float4 A = L.P0[i0 + ii], B = L.P1[i0 + ii];
+      const float2 K = reinterpret_cast<const float2*>(L.P2)[2 * (i0 + ii)];
+      const f2 ex = fma2(HALF, lo(A), PX), ey = fma2(HALF, hi(A), PY), ez = fma2(HALF, lo(B), PZ);
+      const f2 Q = fma2(ez, ez, fma2(ey, ey, fma2(ex, ex, E2)));
+      f2 q[6] = {fma2(ex, TE, Q), fma2(ex, NTE, Q), fma2(ey, TE, Q), fma2(ey, NTE, Q), fma2(ez, TE, Q),
+                 fma2(ez, NTE, Q)};
 #pragma unroll
-      for (int t = 0; t < 6; ++t) v[t][jj] = fmaf(fsqrt(fmaxf(q[t], 1e-6f)), nkappa, kr);
+      for (int t = 0; t < 6; ++t) {
+        if constexpr (CLAMP) q[t] = clamp_q(q[t]);
+        v[t][ii] = fma2(sqrt2(q[t]), NK, f2{K.x, K.y});
+      }
     }
 #pragma unroll
     for (int t = 0; t < 6; ++t) {
-      float cm = v[t][0];
+      float cm = fmaxf(v[t][0].x, v[t][0].y);
 #pragma unroll
-      for (int jj = 1; jj < 8; ++jj) cm = fmaxf(cm, v[t][jj]);
+      for (int ii = 1; ii < 4; ++ii) cm = fmaxf(cm, fmaxf(v[t][ii].x, v[t][ii].y));
       const float mn = fmaxf(m[t], cm);
-      float acc = s[t] * fexp2(m[t] - mn);
+      const f2 MN = sp(mn);
+      f2 acc = f2{s[t] * fexp2(m[t] - mn), 0.0f};
 #pragma unroll
-      for (int jj = 0; jj < 8; ++jj) acc += fexp2(v[t][jj] - mn);
-      s[t] = acc;
+      for (int ii = 0; ii < 4; ++ii) acc += exp2v(v[t][ii] - MN);
+      s[t] = acc.x + acc.y;
       m[t] = mn;
     }
   }
 }
 
-// Shared sweep at p_final: colour softmax over -csharp*delta (renderer_diff.rs:74-82) and
-// the mask soft-min over -k*delta (renderer_diff.rs:86). Both maxima sit at min delta,
-// so one running minimum dmin shifts both sums.
-__device__ __forceinline__ void shade_sweep(float px, float py, float pz, float pp, const Lds& L, int n,
-                                            float c10l, float kappa, float& dmin, float& Zw, float (&C)[3],
-                                            float& Zb) {
-  for (int j0 = 0; j0 < n; j0 += 8) {
-    float dl[8];
+// Distances delta_j = rho_j - r_j at p_final for a pair (shade sweep and backward sweep 1 share it).
+template <bool CLAMP>
+__device__ __forceinline__ f2 delta_pair(const f2& PX, const f2& PY, const f2& PZ, const f2& PP, const float4& A,
+                                         const float4& B, const float4& R, f2& q_out, f2& rho_out) {
+  f2 q = qpair(PX, PY, PZ, PP, A, B);
+  q_out = q;
+  if constexpr (CLAMP) q = clamp_q(q);
+  rho_out = sqrt2(q);
+  return rho_out - hi(R);
+}
+
+// Shared sweep at p_final: colour softmax over -csharp*delta (renderer_diff.rs:74-82) and the mask
+// soft-min over -k*delta (renderer_diff.rs:86). Both maxima sit at min delta, so one running
+// minimum dmin shifts both sums; exponents are (dmin - delta) <= 0 exactly (never overflow).
+template <bool CLAMP>
+__device__ __forceinline__ void shade_sweep(const float p[3], const Lds& L, int npairs, float c10l, float kappa,
+                                            float& dmin, f2& Zw, f2 (&C)[3], f2& Zb) {
+  const f2 PX = sp(p[0]), PY = sp(p[1]), PZ = sp(p[2]), PP = sp(psq(p)), CL = sp(c10l), KA = sp(kappa);
+  for (int i0 = 0; i0 < npairs; i0 += 4) {
+    f2 dl[4];
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      const float4 g = L.geo[j0 + jj];
-      dl[jj] = fsqrt(fmaxf(qexp(px, py, pz, pp, g), 1e-6f)) - L.krr[j0 + jj].y;
+    for (int ii = 0; ii < 4; ++ii) {
+      f2 q, rho;
+      dl[ii] = delta_pair<CLAMP>(PX, PY, PZ, PP, L.P0[i0 + ii], L.P1[i0 + ii], L.P2[i0 + ii], q, rho);
     }
-    float cmin = dl[0];
+    float cmin = fminf(dl[0].x, dl[0].y);
 #pragma unroll
-    for (int jj = 1; jj < 8; ++jj) cmin = fminf(cmin, dl[jj]);
+    for (int ii = 1; ii < 4; ++ii) cmin = fminf(cmin, fminf(dl[ii].x, dl[ii].y));
     const float dn = fminf(dmin, cmin);
-    const float sw = fexp2((dn - dmin) * c10l), sb = fexp2((dn - dmin) * kappa);
+    const f2 sw = sp(fexp2((dn - dmin) * c10l)), sb = sp(fexp2((dn - dmin) * kappa));
     Zw *= sw;
     C[0] *= sw;
     C[1] *= sw;
     C[2] *= sw;
     Zb *= sb;
     dmin = dn;
+    const f2 DN = sp(dn);
 #pragma unroll
-    for (int jj = 0; jj < 8; ++jj) {
-      // (dn - dl) <= 0 exactly: dn is the minimum of these very values, so the exponents can
-      // never overflow however large |p| gets (miss rays march to |p| ~ 1e9 and beyond).
-      const float dd = dn - dl[jj];
-      const float ew = fexp2(dd * c10l);
-      const float eb = fexp2(dd * kappa);
-      const float4 c = L.col[j0 + jj];
+    for (int ii = 0; ii < 4; ++ii) {
+      const f2 dd = DN - dl[ii];
+      const f2 ew = exp2v(dd * CL), eb = exp2v(dd * KA);
+      const float4 c3 = L.P3[i0 + ii];
+      const float2 c4 = L.P4[i0 + ii];
       Zw += ew;
-      C[0] = fmaf(ew, c.x, C[0]);
-      C[1] = fmaf(ew, c.y, C[1]);
-      C[2] = fmaf(ew, c.z, C[2]);
+      C[0] = fma2(ew, lo(c3), C[0]);
+      C[1] = fma2(ew, hi(c3), C[1]);
+      C[2] = fma2(ew, f2{c4.x, c4.y}, C[2]);
       Zb += eb;
     }
   }
@@ -207,13 +275,17 @@ __device__ __forceinline__ void shade_sweep(float px, float py, float pz, float 
 
 // ---- the fused per-ray kernel ----------------------------------------------------------
 template <int MODE, bool CAM>
-__global__ __launch_bounds__(kBlock) void rm_ray_kernel(const KArgs a) {
+__global__ __launch_bounds__(kBlock, 4) void rm_ray_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   Lds L;
-  L.geo = reinterpret_cast<float4*>(smem);
-  L.col = L.geo + a.tile;
-  L.krr = reinterpret_cast<float2*>(L.col + a.tile);
-  L.slots = reinterpret_cast<float*>(L.krr + a.tile);
+  const int tile = a.tile;
+  L.P0 = reinterpret_cast<float4*>(smem);
+  L.P1 = L.P0 + tile / 2;
+  L.P2 = L.P1 + tile / 2;
+  L.P3 = L.P2 + tile / 2;
+  L.P4 = reinterpret_cast<float2*>(L.P3 + tile / 2);
+  L.slots = reinterpret_cast<float*>(L.P4 + tile / 2);
+  L.misc = L.slots + 2 * kWaves * kChunkBwd * 8;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long long li = (long long)blockIdx.x * kBlock + tid;
@@ -221,7 +293,7 @@ __global__ __launch_bounds__(kBlock) void rm_ray_kernel(const KArgs a) {
   const long long ri = a.ray_begin + (valid ? li : 0);
 
   const float kappa = a.k * kLog2e, nkappa = -kappa, inv_kappa = 1.0f / kappa;
-  const bool multi = a.Mpad > a.tile;
+  const bool multi = a.Mpad > tile;
 
   // ray (camera.rs:58-87 in camera mode)
   float o[3], d[3];
@@ -240,14 +312,27 @@ __global__ __launch_bounds__(kBlock) void rm_ray_kernel(const KArgs a) {
     d[2] = a.dir[3 * ri + 2];
   }
 
+  // Minimum sphere radius of the scene (single-tile case): with it, a lower bound on the scene
+  // distance proves rho_j = dist_j + r_j >= kSafeRho for every sphere, so max(q, 1e-6) cannot
+  // bind and the sweeps may skip it (exactly the same results). Multi-tile: fast path off.
+  float rmin = -INFINITY;
   if (!multi) {
-    stage_tile(a, L, 0, a.Mpad, kappa);
+    float rl = stage_tile(a, L, 0, a.Mpad, kappa);
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) rl = fminf(rl, __shfl_xor(rl, off));
+    if (lane == 0) L.misc[wave] = rl;
     __syncthreads();
+    rmin = L.misc[0];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) rmin = fminf(rmin, L.misc[w]);
   }
+  // Wave-uniform choice of the clamp-free path from a per-lane lower bound on the distance.
+  auto all_safe = [&](float dist_lb) { return __all(dist_lb + rmin >= kSafeRho) != 0; };
+
   // Visit every sphere tile (restaging LDS only when M exceeds one tile).
   auto for_tiles = [&](auto&& body) {
-    for (int t0 = 0; t0 < a.Mpad; t0 += a.tile) {
-      const int tn = min(a.tile, a.Mpad - t0);
+    for (int t0 = 0; t0 < a.Mpad; t0 += tile) {
+      const int tn = min(tile, a.Mpad - t0);
       if (multi) {
         __syncthreads();
         stage_tile(a, L, t0, tn, kappa);
@@ -257,23 +342,30 @@ __global__ __launch_bounds__(kBlock) void rm_ray_kernel(const KArgs a) {
     }
   };
   // soft-min scene SDF at one point (scene.rs:60-79 + sdf.rs:30-44); returns D, keeps (m, s)
-  auto soft_min = [&](const float p[3], float& m, float& s) {
-    const float pp = fmaf(p[2], p[2], fmaf(p[1], p[1], p[0] * p[0]));
+  auto soft_min = [&](const float p[3], bool fast, float& m, float& s) {
     m = -INFINITY;
     s = 0.0f;
-    for_tiles([&](int, int tn) { lse_point(p[0], p[1], p[2], pp, L, tn, nkappa, m, s); });
+    if (fast)
+      for_tiles([&](int, int tn) { lse_point<false>(p, L, tn / 2, nkappa, m, s); });
+    else
+      for_tiles([&](int, int tn) { lse_point<true>(p, L, tn / 2, nkappa, m, s); });
     return -(flog2(fmaxf(s, 1e-8f)) + m) * inv_kappa;
   };
 
   // ---- march: t <- (t + sdf(o + d t)).detach(), S times (renderer_diff.rs:20-26)
+  // The fast path needs a distance lower bound: the previous point's hard minimum -m/kappa minus
+  // the step just taken (every dist_j is 1-Lipschitz and |d| = 1).
   float t = 0.0f;
+  float lb = -INFINITY;  // lower bound on the scene distance at the current point
   if (MODE == kBwd && a.t_in != nullptr) {
     t = a.t_in[ri];
   } else {
     for (int st = 0; st < a.steps; ++st) {
       const float p[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
       float m, s;
-      t += soft_min(p, m, s);
+      const float D = soft_min(p, all_safe(lb), m, s);
+      t += D;
+      lb = -m * inv_kappa - fabsf(D);
     }
   }
   if (MODE == kFwd && a.t_out != nullptr && valid) a.t_out[ri] = t;
@@ -281,8 +373,12 @@ __global__ __launch_bounds__(kBlock) void rm_ray_kernel(const KArgs a) {
   // ---- reconnect: t_final = t + sdf(p_approx) (renderer_diff.rs:30-39)
   const float pa[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
   float mA, sA;
-  const float tf = t + soft_min(pa, mA, sA);
+  const bool fast_a = all_safe(lb);
+  const float Da = soft_min(pa, fast_a, mA, sA);
+  const float tf = t + Da;
   const float p[3] = {fmaf(d[0], tf, o[0]), fmaf(d[1], tf, o[1]), fmaf(d[2], tf, o[2])};
+  // p_final is |Da| from p_approx; the taps another eps away
+  const bool fast_f = all_safe(-mA * inv_kappa - fabsf(Da) - a.eps);
 
   // ---- detached 6-tap normal (scene.rs:81-128)
   float nrm[3];
@@ -295,7 +391,10 @@ __global__ __launch_bounds__(kBlock) void rm_ray_kernel(const KArgs a) {
       s6[q] = 0.0f;
     }
     const float eps = a.eps;
-    for_tiles([&](int, int tn) { lse_taps(p, L, tn, nkappa, 2.0f * eps, eps * eps, m6, s6); });
+    if (fast_f)
+      for_tiles([&](int, int tn) { lse_taps<false>(p, L, tn / 2, nkappa, 2.0f * eps, eps * eps, m6, s6); });
+    else
+      for_tiles([&](int, int tn) { lse_taps<true>(p, L, tn / 2, nkappa, 2.0f * eps, eps * eps, m6, s6); });
 #pragma unroll
     for (int q = 0; q < 6; ++q) D6[q] = -(flog2(fmaxf(s6[q], 1e-8f)) + m6[q]) * inv_kappa;
     const float nx = D6[0] - D6[1], ny = D6[2] - D6[3], nz = D6[4] - D6[5];
@@ -316,11 +415,15 @@ __global__ __launch_bounds__(kBlock) void rm_ray_kernel(const KArgs a) {
 
   // ---- colour softmax + mask (renderer_diff.rs:64-90)
   const float c10l = a.csharp * kLog2e;
-  const float pp = fmaf(p[2], p[2], fmaf(p[1], p[1], p[0] * p[0]));
-  float dmin = INFINITY, Zw = 0.0f, Zb = 0.0f, C[3] = {0.0f, 0.0f, 0.0f};
-  for_tiles([&](int, int tn) { shade_sweep(p[0], p[1], p[2], pp, L, tn, c10l, kappa, dmin, Zw, C, Zb); });
+  float dmin = INFINITY;
+  f2 Zw2 = sp(0.0f), Zb2 = sp(0.0f), C2[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
+  if (fast_f)
+    for_tiles([&](int, int tn) { shade_sweep<false>(p, L, tn / 2, c10l, kappa, dmin, Zw2, C2, Zb2); });
+  else
+    for_tiles([&](int, int tn) { shade_sweep<true>(p, L, tn / 2, c10l, kappa, dmin, Zw2, C2, Zb2); });
+  const float Zw = Zw2.x + Zw2.y, Zb = Zb2.x + Zb2.y;
   const float invZw = frcp(Zw);
-  const float mix[3] = {C[0] * invZw, C[1] * invZw, C[2] * invZw};
+  const float mix[3] = {(C2[0].x + C2[0].y) * invZw, (C2[1].x + C2[1].y) * invZw, (C2[2].x + C2[2].y) * invZw};
   const float Df = dmin - flog2(fmaxf(Zb, 1e-8f)) * inv_kappa;
   const float mu = frcp(1.0f + fexp2(a.msharp * kLog2e * Df));  // sigmoid(-msharp * D)
   const float scale = Lgt * mu;
@@ -373,89 +476,129 @@ __global__ __launch_bounds__(kBlock) void rm_ray_kernel(const KArgs a) {
   const float cmu = gmu * mu * (1.0f - mu) * (-a.msharp);
   const float mg = fmaf(mix[2], gm[2], fmaf(mix[1], gm[1], mix[0] * gm[0]));
   const float b_scale = cmu * frcp(Zb);
-  const float ncs = -a.csharp;
 
   float* rec = a.partials + (long long)blockIdx.x * a.rec;
   float* slots = L.slots;
   int chunk_ctr = 0;
 
   // ---- backward sweep 1 at p_final: colour softmax + mask soft-min + p_final(t_final)
-  float gp[3] = {0.0f, 0.0f, 0.0f};
-  for_tiles([&](int t0, int tn) {
-    for (int jc = 0; jc < tn; jc += kChunkBwd, ++chunk_ctr) {
-      float* sb = slots + (chunk_ctr & 1) * (kWaves * kChunkBwd * 8);
-      for (int jj = 0; jj < kChunkBwd; ++jj) {
-        const int j = jc + jj;
-        const float4 gg = L.geo[j];
-        const float2 kr = L.krr[j];
-        const float4 c4 = L.col[j];
-        const float q = qexp(p[0], p[1], p[2], pp, gg);
-        const float rho = fsqrt(fmaxf(q, 1e-6f));  // bitwise the forward's value (shade_sweep)
-        const float dl = rho - kr.y;
-        const float ir = frcp(rho);
-        const float dd = dmin - dl;                 // <= 0 exactly
-        const float w = fexp2(dd * c10l) * invZw;
-        const float bt = fexp2(dd * kappa) * b_scale;
-        const float cg = fmaf(c4.z, gm[2], fmaf(c4.y, gm[1], c4.x * gm[0]));
-        const float gd = fmaf(w * ncs, cg - mg, bt);
-        const float gu = q >= 1e-6f ? gd * ir : 0.0f;  // clamp_min(1e-6) gate
-        const float ex = fmaf(0.5f, gg.x, p[0]), ey = fmaf(0.5f, gg.y, p[1]), ez = fmaf(0.5f, gg.z, p[2]);
-        gp[0] = fmaf(gu, ex, gp[0]);
-        gp[1] = fmaf(gu, ey, gp[1]);
-        gp[2] = fmaf(gu, ez, gp[2]);
-        const float vals[8] = {-gu * ex, -gu * ey, -gu * ez, -gd, w * gm[0], w * gm[1], w * gm[2], 0.0f};
-        const float red = wave_reduce8(vals, lane);
-        if ((lane & 7) == 7) sb[(wave * kChunkBwd + jj) * 8 + (lane >> 3)] = red;
-      }
-      __syncthreads();
-      {
-        const float* s0 = sb + tid;
-        float acc = s0[0];
+  f2 GP[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
+  {
+    const f2 PX = sp(p[0]), PY = sp(p[1]), PZ = sp(p[2]), PP = sp(psq(p)), CL = sp(c10l), KA = sp(kappa),
+             DM = sp(dmin), IZ = sp(invZw), BS = sp(b_scale), G0 = sp(gm[0]), G1 = sp(gm[1]), G2 = sp(gm[2]),
+             MG = sp(mg), NCS = sp(-a.csharp), HALF = sp(0.5f);
+    auto sweep1 = [&](auto clamp_tag, int t0, int tn) {
+      constexpr bool CLAMP = decltype(clamp_tag)::value;
+      for (int jc = 0; jc < tn; jc += kChunkBwd, ++chunk_ctr) {
+        float* sb = slots + (chunk_ctr & 1) * (kWaves * kChunkBwd * 8);
+        for (int jj = 0; jj < kChunkBwd; jj += 4) {  // 4 spheres (2 pairs) per masked LDS write
+          float red[4];
 #pragma unroll
-        for (int w = 1; w < kWaves; ++w) acc += s0[w * kChunkBwd * 8];
-        rec[(long long)(t0 + jc) * 8 + tid] = acc;
+          for (int u = 0; u < 2; ++u) {
+            const int i = (jc + jj) / 2 + u;
+            const float4 A = L.P0[i], B = L.P1[i], R = L.P2[i], C3 = L.P3[i];
+            const float2 C4 = L.P4[i];
+            f2 q, rho;
+            const f2 dl = delta_pair<CLAMP>(PX, PY, PZ, PP, A, B, R, q, rho);  // bitwise the shade sweep's
+            const f2 ir = rcp2(rho);
+            const f2 dd = DM - dl;  // <= 0 exactly
+            const f2 w = exp2v(dd * CL) * IZ;
+            const f2 bt = exp2v(dd * KA) * BS;
+            const f2 cg = fma2(f2{C4.x, C4.y}, G2, fma2(hi(C3), G1, lo(C3) * G0));
+            const f2 gd = fma2(w * NCS, cg - MG, bt);
+            f2 gu = gd * ir;
+            if constexpr (CLAMP) {  // clamp_min(1e-6) gate
+              gu.x = q.x >= 1e-6f ? gu.x : 0.0f;
+              gu.y = q.y >= 1e-6f ? gu.y : 0.0f;
+            }
+            const f2 ex = fma2(HALF, lo(A), PX), ey = fma2(HALF, hi(A), PY), ez = fma2(HALF, lo(B), PZ);
+            GP[0] = fma2(gu, ex, GP[0]);
+            GP[1] = fma2(gu, ey, GP[1]);
+            GP[2] = fma2(gu, ez, GP[2]);
+            const f2 ngu = -gu;
+            const f2 v0 = ngu * ex, v1 = ngu * ey, v2 = ngu * ez, v4 = w * G0, v5 = w * G1, v6 = w * G2;
+            const float va[8] = {v0.x, v1.x, v2.x, -gd.x, v4.x, v5.x, v6.x, 0.0f};
+            const float vb[8] = {v0.y, v1.y, v2.y, -gd.y, v4.y, v5.y, v6.y, 0.0f};
+            red[2 * u] = wave_reduce8(va, lane);
+            red[2 * u + 1] = wave_reduce8(vb, lane);
+          }
+          if ((lane & 7) == 7) {
+            float* dst = sb + (wave * kChunkBwd + jj) * 8 + (lane >> 3);
+#pragma unroll
+            for (int k2 = 0; k2 < 4; ++k2) dst[8 * k2] = red[k2];
+          }
+        }
+        __syncthreads();
+        {
+          const float* s0 = sb + tid;
+          float acc = s0[0];
+#pragma unroll
+          for (int w = 1; w < kWaves; ++w) acc += s0[w * kChunkBwd * 8];
+          rec[(long long)(t0 + jc) * 8 + tid] = acc;
+        }
       }
-    }
-  });
+    };
+    if (fast_f)
+      for_tiles([&](int t0, int tn) { sweep1(std::false_type{}, t0, tn); });
+    else
+      for_tiles([&](int t0, int tn) { sweep1(std::true_type{}, t0, tn); });
+  }
   __syncthreads();
 
   // ---- backward sweep 2 at p_approx: t_final = t + D(p_approx) -> g_t * softmax(-k dist_a)
+  const float gp[3] = {GP[0].x + GP[0].y, GP[1].x + GP[1].y, GP[2].x + GP[2].y};
   const float gt = fmaf(gp[2], d[2], fmaf(gp[1], d[1], gp[0] * d[0]));
-  const float hsc = gt * frcp(sA);
-  const float ppa = fmaf(pa[2], pa[2], fmaf(pa[1], pa[1], pa[0] * pa[0]));
-  for_tiles([&](int t0, int tn) {
-    for (int jc = 0; jc < tn; jc += kChunkBwd, ++chunk_ctr) {
-      float* sb = slots + (chunk_ctr & 1) * (kWaves * kChunkBwd * 8);
-      for (int jj = 0; jj < kChunkBwd; jj += 2) {
-        float vals[8];
+  {
+    const f2 PX = sp(pa[0]), PY = sp(pa[1]), PZ = sp(pa[2]), PP = sp(psq(pa)), NK = sp(nkappa), MA = sp(mA),
+             HS = sp(gt * frcp(sA)), HALF = sp(0.5f);
+    auto sweep2 = [&](auto clamp_tag, int t0, int tn) {
+      constexpr bool CLAMP = decltype(clamp_tag)::value;
+      for (int jc = 0; jc < tn; jc += kChunkBwd, ++chunk_ctr) {
+        float* sb = slots + (chunk_ctr & 1) * (kWaves * kChunkBwd * 8);
+        for (int jj = 0; jj < kChunkBwd; jj += 4) {  // 2 pairs per masked LDS write
+          float red[2];
 #pragma unroll
-        for (int u = 0; u < 2; ++u) {
-          const int j = jc + jj + u;
-          const float4 gg = L.geo[j];
-          const float kr = L.krr[j].x;
-          const float q = qexp(pa[0], pa[1], pa[2], ppa, gg);
-          const float rho = fsqrt(fmaxf(q, 1e-6f));  // bitwise the reconnect sweep's value
-          const float ir = frcp(rho);
-          const float h = fexp2(fmaf(rho, nkappa, kr) - mA) * hsc;  // v - mA <= 0 exactly
-          const float hu = q >= 1e-6f ? h * ir : 0.0f;
-          vals[4 * u + 0] = -hu * fmaf(0.5f, gg.x, pa[0]);
-          vals[4 * u + 1] = -hu * fmaf(0.5f, gg.y, pa[1]);
-          vals[4 * u + 2] = -hu * fmaf(0.5f, gg.z, pa[2]);
-          vals[4 * u + 3] = -h;
+          for (int u = 0; u < 2; ++u) {
+            const int i = (jc + jj) / 2 + u;
+            const float4 A = L.P0[i], B = L.P1[i];
+            const float2 K = reinterpret_cast<const float2*>(L.P2)[2 * i];
+            f2 q = qpair(PX, PY, PZ, PP, A, B);  // bitwise the reconnect sweep's q
+            const f2 qraw = q;
+            if constexpr (CLAMP) q = clamp_q(q);
+            const f2 rho = sqrt2(q);
+            const f2 h = exp2v(fma2(rho, NK, f2{K.x, K.y}) - MA) * HS;  // v - mA <= 0 exactly
+            f2 hu = h * rcp2(rho);
+            if constexpr (CLAMP) {
+              hu.x = qraw.x >= 1e-6f ? hu.x : 0.0f;
+              hu.y = qraw.y >= 1e-6f ? hu.y : 0.0f;
+            }
+            const f2 nhu = -hu;
+            const f2 v0 = nhu * fma2(HALF, lo(A), PX), v1 = nhu * fma2(HALF, hi(A), PY),
+                     v2 = nhu * fma2(HALF, lo(B), PZ);
+            const float vals[8] = {v0.x, v1.x, v2.x, -h.x, v0.y, v1.y, v2.y, -h.y};
+            red[u] = wave_reduce8(vals, lane);
+          }
+          if ((lane & 7) == 7) {
+            float* dst = sb + (wave * kChunkBwd + jj) * 4 + (lane >> 3);
+            dst[0] = red[0];
+            dst[8] = red[1];
+          }
         }
-        const float red = wave_reduce8(vals, lane);
-        if ((lane & 7) == 7) sb[(wave * kChunkBwd + jj) * 4 + (lane >> 3)] = red;
-      }
-      __syncthreads();
-      if (tid < kChunkBwd * 4) {
-        const float* s0 = sb + tid;
-        float acc = s0[0];
+        __syncthreads();
+        if (tid < kChunkBwd * 4) {
+          const float* s0 = sb + tid;
+          float acc = s0[0];
 #pragma unroll
-        for (int w = 1; w < kWaves; ++w) acc += s0[w * kChunkBwd * 4];
-        rec[(long long)a.Mpad * 8 + (long long)(t0 + jc) * 4 + tid] = acc;
+          for (int w = 1; w < kWaves; ++w) acc += s0[w * kChunkBwd * 4];
+          rec[(long long)a.Mpad * 8 + (long long)(t0 + jc) * 4 + tid] = acc;
+        }
       }
-    }
-  });
+    };
+    if (fast_a)
+      for_tiles([&](int t0, int tn) { sweep2(std::false_type{}, t0, tn); });
+    else
+      for_tiles([&](int t0, int tn) { sweep2(std::true_type{}, t0, tn); });
+  }
   __syncthreads();
 
   // ---- per-ray scalars: light (pre-projection), ambient, loss
@@ -474,69 +617,107 @@ __global__ __launch_bounds__(kBlock) void rm_ray_kernel(const KArgs a) {
 }
 
 // ---- cross-block reduction (fixed order => deterministic) --------------------------------
-// Pass 1: S[seg][col] = sum over blocks b in segment seg of P[b][col].
-__global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restrict__ P, long long rec,
+// Partial record of one ray block (rec = Mpad*12 + 8 floats):
+//   [Mpad][8] sweep 1 (gc.xyz, gr, gcol.rgb, 0) | [Mpad][4] sweep 2 (gc.xyz, gr) | 8 scalars
+// Output columns (ncols = Mpad*8 + 8): [Mpad][8] combined per-sphere grads | 8 scalars.
+// Pass 1: S[seg][col] = sum over blocks of segment seg (sweep-2 terms folded into their column).
+// Four independent accumulators keep four loads in flight per thread; their combine order is
+// fixed, so results stay bitwise reproducible.
+__global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restrict__ P, long long rec, int Mpad,
                                                           int nblocks, int seg_len, float* __restrict__ S) {
-  const long long col = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (col >= rec) return;
+  const int ncols = Mpad * 8 + 8;
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= ncols) return;
+  long long c1, c2 = -1;
+  if (col < Mpad * 8) {
+    c1 = col;
+    const int j = col >> 3, comp = col & 7;
+    if (comp < 4) c2 = (long long)Mpad * 8 + (long long)j * 4 + comp;
+  } else {
+    c1 = (long long)Mpad * 12 + (col - Mpad * 8);
+  }
   const int b0 = blockIdx.y * seg_len;
   const int b1 = min(b0 + seg_len, nblocks);
-  float acc = 0.0f;
-  for (int b = b0; b < b1; ++b) acc += P[(long long)b * rec + col];
-  S[(long long)blockIdx.y * rec + col] = acc;
+  float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+  int b = b0;
+  if (c2 >= 0) {
+    for (; b + 1 < b1; b += 2) {
+      const float* r0 = P + (long long)b * rec;
+      const float* r1 = r0 + rec;
+      a0 += r0[c1];
+      a1 += r0[c2];
+      a2 += r1[c1];
+      a3 += r1[c2];
+    }
+    for (; b < b1; ++b) {
+      a0 += P[(long long)b * rec + c1];
+      a1 += P[(long long)b * rec + c2];
+    }
+  } else {
+    for (; b + 3 < b1; b += 4) {
+      const float* r0 = P + (long long)b * rec + c1;
+      a0 += r0[0];
+      a1 += r0[rec];
+      a2 += r0[2 * rec];
+      a3 += r0[3 * rec];
+    }
+    for (; b < b1; ++b) a0 += P[(long long)b * rec + c1];
+  }
+  S[(long long)blockIdx.y * ncols + col] = (a0 + a1) + (a2 + a3);
 }
 
 // Pass 2: sum the segments in order and scatter into the caller's gradient layout.
 // gld = (g_ell - ldn (ldn . g_ell)) / |ld| applies the Jacobian of ld / |ld| (renderer_diff.rs:49-50).
-__global__ __launch_bounds__(256) void rm_finalize_grads(const float* __restrict__ S, long long rec, int nseg,
-                                                         int M, int Mpad, const float* __restrict__ light_dir,
-                                                         float* gc, float* gcol, float* gr, float* gld, float* gamb,
-                                                         float* loss_sum, int accumulate) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  if (j < M) {
-    float v[12];
-#pragma unroll
-    for (int c = 0; c < 12; ++c) v[c] = 0.0f;
-    for (int s = 0; s < nseg; ++s) {
-      const float* r1 = S + (long long)s * rec + (long long)j * 8;
-      const float* r2 = S + (long long)s * rec + (long long)Mpad * 8 + (long long)j * 4;
-#pragma unroll
-      for (int c = 0; c < 8; ++c) v[c] += r1[c];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) v[8 + c] += r2[c];
-    }
-    const float gcv[3] = {v[0] + v[8], v[1] + v[9], v[2] + v[10]};
-    const float grv = v[3] + v[11];
-    if (gc) {
-#pragma unroll
-      for (int c = 0; c < 3; ++c) gc[3 * j + c] = accumulate ? gc[3 * j + c] + gcv[c] : gcv[c];
-    }
-    if (gr) gr[j] = accumulate ? gr[j] + grv : grv;
-    if (gcol) {
-#pragma unroll
-      for (int c = 0; c < 3; ++c) gcol[3 * j + c] = accumulate ? gcol[3 * j + c] + v[4 + c] : v[4 + c];
-    }
+__device__ __forceinline__ float sum_segments(const float* __restrict__ S, int ncols, int nseg, int col) {
+  float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
+  int s = 0;
+  for (; s + 3 < nseg; s += 4) {
+    const float* r = S + (long long)s * ncols + col;
+    a0 += r[0];
+    a1 += r[ncols];
+    a2 += r[2 * ncols];
+    a3 += r[3 * ncols];
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    float r[5] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    for (int s = 0; s < nseg; ++s) {
-      const float* r0 = S + (long long)s * rec + (long long)Mpad * 12;
-#pragma unroll
-      for (int c = 0; c < 5; ++c) r[c] += r0[c];
-    }
+  for (; s < nseg; ++s) a0 += S[(long long)s * ncols + col];
+  return (a0 + a1) + (a2 + a3);
+}
+
+__global__ __launch_bounds__(256) void rm_finalize_grads(const float* __restrict__ S, int nseg, int M, int Mpad,
+                                                         const float* __restrict__ light_dir, float* gc,
+                                                         float* gcol, float* gr, float* gld, float* gamb,
+                                                         float* loss_sum, int accumulate) {
+  const int ncols = Mpad * 8 + 8;
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= ncols) return;
+  if (col < Mpad * 8) {
+    const int j = col >> 3, comp = col & 7;
+    if (j >= M || comp == 7) return;
+    const float v = sum_segments(S, ncols, nseg, col);
+    float* dst = comp < 3 ? (gc ? gc + 3 * j + comp : nullptr)
+                          : (comp == 3 ? (gr ? gr + j : nullptr) : (gcol ? gcol + 3 * j + (comp - 4) : nullptr));
+    if (dst) *dst = accumulate ? *dst + v : v;
+    return;
+  }
+  const int sc = col - Mpad * 8;
+  if (sc == 0 && gld) {
+    const float r0 = sum_segments(S, ncols, nseg, col), r1 = sum_segments(S, ncols, nseg, col + 1),
+                r2 = sum_segments(S, ncols, nseg, col + 2);
     const float l0 = light_dir[0], l1 = light_dir[1], l2 = light_dir[2];
     const float len = sqrtf(l0 * l0 + l1 * l1 + l2 * l2);
     const float ln[3] = {l0 / len, l1 / len, l2 / len};
-    const float proj = ln[0] * r[0] + ln[1] * r[1] + ln[2] * r[2];
-    if (gld) {
+    const float r[3] = {r0, r1, r2};
+    const float proj = ln[0] * r0 + ln[1] * r1 + ln[2] * r2;
 #pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const float gv = (r[c] - ln[c] * proj) / len;
-        gld[c] = accumulate ? gld[c] + gv : gv;
-      }
+    for (int c = 0; c < 3; ++c) {
+      const float gv = (r[c] - ln[c] * proj) / len;
+      gld[c] = accumulate ? gld[c] + gv : gv;
     }
-    if (gamb) gamb[0] = accumulate ? gamb[0] + r[3] : r[3];
-    if (loss_sum) loss_sum[0] = accumulate ? loss_sum[0] + r[4] : r[4];
+  } else if (sc == 3 && gamb) {
+    const float v = sum_segments(S, ncols, nseg, col);
+    gamb[0] = accumulate ? gamb[0] + v : v;
+  } else if (sc == 4 && loss_sum) {
+    const float v = sum_segments(S, ncols, nseg, col);
+    loss_sum[0] = accumulate ? loss_sum[0] + v : v;
   }
 }
 
@@ -545,99 +726,133 @@ __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf
 // burn::tensor::activation::softplus(x, 1) = log(1 + exp(x))
 __device__ __forceinline__ float softplusf_(float x) { return logf(1.0f + expf(x)); }
 
+// scene.rs:41-45 on packed element i (layout [centers 3M | colors 3M | radius M | light 3 | ambient 1]).
+__device__ __forceinline__ float activate_elem(float x, int i, int M) {
+  if (i < 3 * M) return x;                           // centers
+  if (i < 6 * M) return sigmoidf_(x);                // colors = sigmoid(raw)        scene.rs:41
+  if (i < 7 * M) return softplusf_(x) + 0.01f;       // radius = softplus(raw)+0.01  scene.rs:43
+  if (i < 7 * M + 3) return x;                       // light_dir raw                scene.rs:44
+  return sigmoidf_(x);                               // ambient = sigmoid(raw)       scene.rs:45
+}
+
 __global__ __launch_bounds__(256) void rm_activate_kernel(const float* __restrict__ raw, int M,
                                                           float* __restrict__ act) {
   const int i = blockIdx.x * 256 + threadIdx.x;
-  const int n = 7 * M + 4;
-  if (i >= n) return;
-  const float x = raw[i];
-  float y;
-  if (i < 3 * M) y = x;                       // centers
-  else if (i < 6 * M) y = sigmoidf_(x);       // colors = sigmoid(raw)      scene.rs:41
-  else if (i < 7 * M) y = softplusf_(x) + 0.01f;  // radius = softplus+0.01  scene.rs:43
-  else if (i < 7 * M + 3) y = x;              // light_dir raw               scene.rs:44
-  else y = sigmoidf_(x);                      // ambient = sigmoid(raw)      scene.rs:45
-  act[i] = y;
+  if (i >= 7 * M + 4) return;
+  act[i] = activate_elem(raw[i], i, M);
 }
 
-// One thread per parameter element: chain rule of the activations, the compute_loss penalties
-// (training.rs:38-82; O(M) per center element for the repulsion row), coupled weight decay and
-// Burn's Adam update. Penalty value: block 0 reduces; O(M^2) repulsion summed by the threads
-// of the center rows.
+// Block reduction of 4 floats over 256 threads in fixed tree order (deterministic).
+__device__ __forceinline__ void block_sum4(float (&v)[4], float* red) {
+#pragma unroll
+  for (int c = 0; c < 4; ++c) red[c * 256 + threadIdx.x] = v[c];
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (threadIdx.x < w) {
+#pragma unroll
+      for (int c = 0; c < 4; ++c) red[c * 256 + threadIdx.x] += red[c * 256 + threadIdx.x + w];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) v[c] = red[c * 256];
+}
+
+// Pass A of the optimizer: block s owns sphere s. It snapshots the sphere's raw parameters
+// (the update kernel reads neighbours' pre-step values) and, with penalties, sums the
+// repulsion row of training.rs:73-82 over j: dist_ij = sqrt(max(|c_i|^2 + |c_j|^2 - 2 c_i.c_j,
+// 1e-6)), value (dist + 100 I + 1e-6)^-1, gradient through both (s, j) and (j, s) entries.
+__global__ __launch_bounds__(256) void rm_penalty_pairs(const float* __restrict__ raw, int M, int with_pen,
+                                                        float* __restrict__ snap, float* __restrict__ pair) {
+  __shared__ float red[4 * 256];
+  const int s = blockIdx.x;
+  if (threadIdx.x < 7) {
+    const int idx = threadIdx.x < 3 ? 3 * s + threadIdx.x
+                                    : (threadIdx.x < 6 ? 3 * M + 3 * s + (threadIdx.x - 3) : 6 * M + s);
+    snap[idx] = raw[idx];
+  }
+  if (s == 0 && threadIdx.x >= 32 && threadIdx.x < 36) snap[7 * M + threadIdx.x - 32] = raw[7 * M + threadIdx.x - 32];
+  if (!with_pen) return;
+  const float cx = raw[3 * s], cy = raw[3 * s + 1], cz = raw[3 * s + 2];
+  const float csq = cx * cx + cy * cy + cz * cz;
+  float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int j = threadIdx.x; j < M; j += 256) {
+    const float ox = raw[3 * j], oy = raw[3 * j + 1], oz = raw[3 * j + 2];
+    const float q = (csq + (ox * ox + oy * oy + oz * oz)) - (cx * ox + cy * oy + cz * oz) * 2.0f;
+    const float rho = sqrtf(fmaxf(q, 1e-6f));
+    const float den = rho + (j == s ? 100.0f : 0.0f) + 1e-6f;
+    v[3] += 1.0f / den;
+    if (j != s && q >= 1e-6f) {  // clamp_min(1e-6) gate (the diagonal has q ~ 0)
+      const float gs = -2.0f / (den * den) / rho;
+      v[0] += gs * (cx - ox);
+      v[1] += gs * (cy - oy);
+      v[2] += gs * (cz - oz);
+    }
+  }
+  block_sum4(v, red);
+  if (threadIdx.x < 4) pair[4 * s + threadIdx.x] = v[threadIdx.x];
+}
+
+// Pass B: one thread per parameter element: chain rule of the activations, the compute_loss
+// penalties (training.rs:38-82), coupled weight decay and Burn's Adam; optionally writes the
+// activated parameters of the updated model (scene.rs:41-45) for the next step's render.
 __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restrict__ raw, float* __restrict__ raw_out,
                                                            const float* __restrict__ gact,
-                                                           float* __restrict__ m1, float* __restrict__ m2, int M,
-                                                           int step, float lr, float wd, int with_pen,
-                                                           float* __restrict__ pen_parts) {
+                                                           float* __restrict__ m1, float* __restrict__ m2,
+                                                           const float* __restrict__ pair, int M, int step,
+                                                           float lr, float wd, int with_pen,
+                                                           float* __restrict__ pen_parts,
+                                                           float* __restrict__ act_out) {
+  __shared__ float red[4 * 256];
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int n = 7 * M + 4;
   float pen = 0.0f;
   if (i < n) {
     const float x = raw[i];
     float gv = gact[i];
+    const float invM = 1.0f / (float)M;
+    const float rep_scale = 1e-5f / ((float)M * (float)M);
     if (i < 3 * M) {  // centers (identity activation)
       if (with_pen) {
         const int s = i / 3, ax = i - 3 * s;
         const float cx = raw[3 * s], cy = raw[3 * s + 1], cz = raw[3 * s + 2];
         const float rs = softplusf_(raw[6 * M + s]);  // penalties use softplus without +0.01 (training.rs:41)
-        // [b] center attraction: mean(c^2) over [M,3] * 0.05
-        gv += 0.05f * 2.0f * x / (3.0f * M);
-        // [c] camera-proximity barrier: mean(mask * (|c| + r - 1.2)^2) * 5
+        gv += 0.05f * 2.0f * x / (3.0f * M);          // [b] mean(c^2) over [M,3] * 0.05
         const float csq = cx * cx + cy * cy + cz * cz;
         const float dist = sqrtf(csq + 1e-6f);
-        const float reach = dist + rs;
-        if (reach > 1.2f) gv += 5.0f / M * 2.0f * (reach - 1.2f) * (x / dist);
-        // [d] repulsion: mean((dist_ij + 100 I + 1e-6)^-1) * 1e-5 over [M,M]; d/dc_s of both (s,j) and (j,s)
-        float acc = 0.0f;
-        for (int j = 0; j < M; ++j) {
-          const float ox = raw[3 * j], oy = raw[3 * j + 1], oz = raw[3 * j + 2];
-          const float q = (csq + (ox * ox + oy * oy + oz * oz)) - (cx * ox + cy * oy + cz * oz) * 2.0f;
-          if (j == s || q < 1e-6f) continue;  // clamp_min(1e-6) gate; diagonal: q ~ 0
-          const float rho = sqrtf(q);
-          const float den = rho + 1e-6f;
-          const float xo = ax == 0 ? ox : (ax == 1 ? oy : oz);
-          acc += -2.0f / (den * den) * (x - xo) / rho;
-        }
-        gv += 1e-5f / ((float)M * (float)M) * acc;
-        if (ax == 0) {  // penalty value, once per sphere
+        const float reach = dist + rs;                // [c] mean(mask * (|c| + r - 1.2)^2) * 5
+        if (reach > 1.2f) gv += 5.0f * invM * 2.0f * (reach - 1.2f) * (x / dist);
+        gv += rep_scale * pair[4 * s + ax];           // [d] repulsion (rm_penalty_pairs)
+        if (ax == 0) {
           pen += 0.05f * csq / (3.0f * M);
-          if (reach > 1.2f) pen += 5.0f / M * (reach - 1.2f) * (reach - 1.2f);
-          float rep = 0.0f;
-          for (int j = 0; j < M; ++j) {
-            const float ox = raw[3 * j], oy = raw[3 * j + 1], oz = raw[3 * j + 2];
-            const float q = (csq + (ox * ox + oy * oy + oz * oz)) - (cx * ox + cy * oy + cz * oz) * 2.0f;
-            const float rho = sqrtf(fmaxf(q, 1e-6f));
-            rep += 1.0f / (rho + (j == s ? 100.0f : 0.0f) + 1e-6f);
-          }
-          pen += 1e-5f / ((float)M * (float)M) * rep;
+          if (reach > 1.2f) pen += 5.0f * invM * (reach - 1.2f) * (reach - 1.2f);
+          pen += rep_scale * pair[4 * s + 3];
         }
       }
     } else if (i < 6 * M) {  // colors: d sigmoid = c (1 - c)
       const float c = sigmoidf_(x);
       gv *= c * (1.0f - c);
-    } else if (i < 7 * M) {  // radius: d softplus = sigmoid
+    } else if (i < 7 * M) {  // radius: d (softplus + 0.01) = sigmoid
       const float sg = sigmoidf_(x);
       gv *= sg;
       if (with_pen) {
         const int s = i - 6 * M;
         const float rs = softplusf_(x);
-        gv += 0.002f / M * (rs > 0.0f ? 1.0f : (rs < 0.0f ? -1.0f : 0.0f)) * sg;  // [a] L1
-        pen += 0.002f / M * fabsf(rs);
-        if (rs > 1.0f) {  // [a] large-radius
-          gv += 0.04f / M * 2.0f * rs * sg;
-          pen += 0.04f / M * rs * rs;
+        gv += 0.002f * invM * (rs > 0.0f ? 1.0f : (rs < 0.0f ? -1.0f : 0.0f)) * sg;  // [a] L1
+        pen += 0.002f * invM * fabsf(rs);
+        if (rs > 1.0f) {  // [a] large radius
+          gv += 0.04f * invM * 2.0f * rs * sg;
+          pen += 0.04f * invM * rs * rs;
         }
         const float cx = raw[3 * s], cy = raw[3 * s + 1], cz = raw[3 * s + 2];
         const float reach = sqrtf(cx * cx + cy * cy + cz * cz + 1e-6f) + rs;
-        if (reach > 1.2f) gv += 5.0f / M * 2.0f * (reach - 1.2f) * sg;  // [c] wrt radius
+        if (reach > 1.2f) gv += 5.0f * invM * 2.0f * (reach - 1.2f) * sg;  // [c] w.r.t. radius
       }
-    } else if (i < 7 * M + 3) {
-      // light_dir raw: identity
-    } else {  // ambient: d sigmoid
+    } else if (i >= 7 * M + 3) {  // ambient: d sigmoid (light_dir raw: identity)
       const float a = sigmoidf_(x);
       gv *= a * (1.0f - a);
     }
-    // Burn Adam with coupled weight decay: g += wd * theta; m, v moments; bias correction.
+    // Burn Adam with coupled weight decay: g += wd * theta; moments; bias correction.
     gv = fmaf(wd, x, gv);
     const float b1 = 0.9f, b2 = 0.999f, eps = 1e-5f;
     const float mm = fmaf(b1, m1[i], (1.0f - b1) * gv);
@@ -646,17 +861,14 @@ __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restri
     m2[i] = vv;
     const float mh = mm / (1.0f - powf(b1, (float)step));
     const float vh = vv / (1.0f - powf(b2, (float)step));
-    raw_out[i] = x - lr * (mh / (sqrtf(vh) + eps));
+    const float xn = x - lr * (mh / (sqrtf(vh) + eps));
+    raw_out[i] = xn;
+    if (act_out) act_out[i] = activate_elem(xn, i, M);
   }
   if (pen_parts != nullptr) {
-    __shared__ float red[256];
-    red[threadIdx.x] = pen;
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-      if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-      __syncthreads();
-    }
-    if (threadIdx.x == 0) pen_parts[blockIdx.x] = red[0];
+    float v[4] = {pen, 0.0f, 0.0f, 0.0f};
+    block_sum4(v, red);
+    if (threadIdx.x == 0) pen_parts[blockIdx.x] = v[0];
   }
 }
 
@@ -679,6 +891,9 @@ struct rm_context {
   std::string err;
   void* ws = nullptr;  // partials | segment sums | small scratch
   size_t ws_bytes = 0;
+  bool timing = false;  // record hipEvents around every per-ray kernel launch
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
+  size_t events_used = 0;
 };
 
 namespace {
@@ -869,7 +1084,7 @@ int run(rm_context* ctx, const Call& c) {
   a.inv_count = c.inv_count;
   a.dbg = c.dbg;
   a.rec = rec_floats(Mpad);
-  const size_t lds = (size_t)tile * (16 + 16 + 8) + (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float);
+  const size_t lds = lds_bytes(tile);
 
   if (c.mode != kFwd) {
     if ((rc = ensure_ws(ctx, ws_need(std::max<long long>(n, 1), M))) != RM_OK) return rc;
@@ -889,31 +1104,46 @@ int run(rm_context* ctx, const Call& c) {
     a.n_rays = nr;
     a.partials = P;
     if (nb > 0) {
+      hipEvent_t ev0 = nullptr, ev1 = nullptr;
+      if (ctx->timing) {
+        if (ctx->events_used == ctx->events.size()) {
+          std::pair<hipEvent_t, hipEvent_t> pr;
+          RM_HIP(ctx, hipEventCreate(&pr.first));
+          RM_HIP(ctx, hipEventCreate(&pr.second));
+          ctx->events.push_back(pr);
+        }
+        ev0 = ctx->events[ctx->events_used].first;
+        ev1 = ctx->events[ctx->events_used].second;
+        ++ctx->events_used;
+        RM_HIP(ctx, hipEventRecord(ev0, ctx->stream));
+      }
       dim3 grid((unsigned)nb);
       if (c.mode == kFwd) launch_ray<kFwd>(c.cam, grid, lds, ctx->stream, a);
       else if (c.mode == kBwd) launch_ray<kBwd>(c.cam, grid, lds, ctx->stream, a);
       else launch_ray<kTrain>(c.cam, grid, lds, ctx->stream, a);
       RM_HIP(ctx, hipGetLastError());
+      if (ev1) RM_HIP(ctx, hipEventRecord(ev1, ctx->stream));
     }
     if (c.mode != kFwd) {
       const int nblocks = (int)nb;
+      const int ncols = Mpad * 8 + 8;
       float* S = P + (long long)std::max<long long>(nb, 1) * a.rec;
       int segs = std::min(kReduceSegs, std::max(nblocks, 1));
       const int seg_len = nblocks > 0 ? (nblocks + segs - 1) / segs : 0;
       if (nblocks > 0) segs = (nblocks + seg_len - 1) / seg_len;
       if (nblocks > 0) {
-        dim3 g1((unsigned)((a.rec + 255) / 256), (unsigned)segs);
-        hipLaunchKernelGGL(rm_reduce_partials, g1, dim3(256), 0, ctx->stream, P, a.rec, nblocks, seg_len, S);
+        dim3 g1((unsigned)((ncols + 255) / 256), (unsigned)segs);
+        hipLaunchKernelGGL(rm_reduce_partials, g1, dim3(256), 0, ctx->stream, P, a.rec, Mpad, nblocks, seg_len, S);
         RM_HIP(ctx, hipGetLastError());
       } else {
-        RM_HIP(ctx, hipMemsetAsync(S, 0, sizeof(float) * a.rec, ctx->stream));
+        RM_HIP(ctx, hipMemsetAsync(S, 0, sizeof(float) * ncols, ctx->stream));
         segs = 1;
       }
       const rm_grads* gp = c.grads;
       const int acc = (first ? c.accumulate : 1);
-      hipLaunchKernelGGL(rm_finalize_grads, dim3((M + 255) / 256), dim3(256), 0, ctx->stream, S, a.rec, segs, M,
-                         Mpad, c.scene->light_dir, gp->centers, gp->colors, gp->radius, gp->light_dir,
-                         gp->ambient, c.mode == kTrain ? c.loss_sum : nullptr, acc);
+      hipLaunchKernelGGL(rm_finalize_grads, dim3((ncols + 255) / 256), dim3(256), 0, ctx->stream, S, segs, M, Mpad,
+                         c.scene->light_dir, gp->centers, gp->colors, gp->radius, gp->light_dir, gp->ambient,
+                         c.mode == kTrain ? c.loss_sum : nullptr, acc);
       RM_HIP(ctx, hipGetLastError());
     }
     done += nr;
@@ -947,8 +1177,40 @@ int rm_set_stream(rm_context* ctx, void* stream) {
   return RM_OK;
 }
 
+int rm_timing_enable(rm_context* ctx, int32_t enable) {
+  if (!ctx) return RM_ERR_INVALID_ARG;
+  ctx->timing = enable != 0;
+  // pre-create a pool so event creation stays out of timed regions
+  while (ctx->timing && ctx->events.size() < 256) {
+    std::pair<hipEvent_t, hipEvent_t> pr;
+    RM_HIP(ctx, hipEventCreate(&pr.first));
+    RM_HIP(ctx, hipEventCreate(&pr.second));
+    ctx->events.push_back(pr);
+  }
+  return RM_OK;
+}
+
+int rm_timing_collect(rm_context* ctx, double* total_ms, int64_t* launches, int32_t reset) {
+  if (!ctx || !total_ms || !launches) return RM_ERR_INVALID_ARG;
+  double acc = 0.0;
+  for (size_t i = 0; i < ctx->events_used; ++i) {
+    RM_HIP(ctx, hipEventSynchronize(ctx->events[i].second));
+    float ms = 0.0f;
+    RM_HIP(ctx, hipEventElapsedTime(&ms, ctx->events[i].first, ctx->events[i].second));
+    acc += ms;
+  }
+  *total_ms = acc;
+  *launches = (int64_t)ctx->events_used;
+  if (reset) ctx->events_used = 0;
+  return RM_OK;
+}
+
 void rm_destroy(rm_context* ctx) {
   if (!ctx) return;
+  for (auto& pr : ctx->events) {
+    (void)hipEventDestroy(pr.first);
+    (void)hipEventDestroy(pr.second);
+  }
   if (ctx->ws) {
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipFree(ctx->ws);
@@ -1134,24 +1396,28 @@ void rm_grads_from_packed(float* g, int32_t M, rm_grads* o) {
 
 int rm_optimizer_step(rm_context* ctx, float* raw_packed, const float* grad_act_packed, float* adam_m,
                       float* adam_v, int32_t num_spheres, int32_t step, float lr, float weight_decay,
-                      int32_t with_penalties, float* loss_penalty) {
+                      int32_t with_penalties, float* loss_penalty, float* act_out) {
   if (!ctx) return RM_ERR_INVALID_ARG;
   if (!raw_packed || !grad_act_packed || !adam_m || !adam_v)
     return fail(ctx, RM_ERR_INVALID_ARG, "NULL optimizer buffer");
   if (num_spheres < 1 || num_spheres > RM_MAX_SPHERES) return fail(ctx, RM_ERR_INVALID_ARG, "bad num_spheres");
   if (step < 1) return fail(ctx, RM_ERR_INVALID_ARG, "step counts from 1");
-  const int n = 7 * num_spheres + 4;
+  const int M = num_spheres;
+  const int n = 7 * M + 4;
   const int nb = (n + 255) / 256;
-  // The penalties read every sphere's pre-step center while the update writes raw_packed:
-  // the kernel reads a snapshot taken on the stream and writes raw_packed.
-  const size_t need = ((size_t)n + (size_t)nb + 64) * sizeof(float);
+  // workspace: snapshot of the pre-step params | repulsion rows [M][4] | penalty partials
+  const size_t need = ((size_t)n + 4 * (size_t)M + (size_t)nb + 64) * sizeof(float);
   int rc = ensure_ws(ctx, std::max(ctx->ws_bytes, need));
   if (rc != RM_OK) return rc;
   float* snap = static_cast<float*>(ctx->ws);
-  float* parts = loss_penalty ? snap + n : nullptr;
-  RM_HIP(ctx, hipMemcpyAsync(snap, raw_packed, sizeof(float) * n, hipMemcpyDeviceToDevice, ctx->stream));
+  float* pair = snap + n;
+  float* parts = loss_penalty ? pair + 4 * M : nullptr;
+  hipLaunchKernelGGL(rm::rm_penalty_pairs, dim3(M), dim3(256), 0, ctx->stream, raw_packed, M,
+                     with_penalties ? 1 : 0, snap, pair);
+  RM_HIP(ctx, hipGetLastError());
   hipLaunchKernelGGL(rm::rm_optimizer_kernel, dim3(nb), dim3(256), 0, ctx->stream, snap, raw_packed,
-                     grad_act_packed, adam_m, adam_v, num_spheres, step, lr, weight_decay, with_penalties, parts);
+                     grad_act_packed, adam_m, adam_v, pair, M, step, lr, weight_decay, with_penalties ? 1 : 0, parts,
+                     act_out);
   RM_HIP(ctx, hipGetLastError());
   if (loss_penalty) {
     hipLaunchKernelGGL(rm::rm_sum_small, dim3(1), dim3(64), 0, ctx->stream, parts, nb, loss_penalty);

@@ -58,6 +58,7 @@ class SceneModel:
         self.raw = raw_packed.contiguous().float()
         self.num_spheres = num_spheres
         self._act = torch.empty_like(self.raw)
+        self._act_valid = False  # _act == activate(raw); Adam.step keeps it valid
 
     @classmethod
     def from_raw(cls, centers, colors, radius, light_dir, ambient, device="cuda"):
@@ -70,10 +71,17 @@ class SceneModel:
         return cls.from_raw(centers, logit(colors), softplus_inv(np.asarray(radius, np.float64) - 0.01), light_dir,
                             logit(ambient), device=device)
 
+    def invalidate(self):
+        """Call after modifying ``raw`` outside the optimizer."""
+        self._act_valid = False
+
     def activated_packed(self) -> torch.Tensor:
-        ctx = context(self.raw.device)
-        ctx.check(ctx._lib.rm_scene_activate(ctx.handle, ctypes.c_void_p(self.raw.data_ptr()), self.num_spheres,
-                                             ctypes.c_void_p(self._act.data_ptr())), "rm_scene_activate")
+        if not self._act_valid:
+            ctx = context(self.raw.device)
+            ctx.check(ctx._lib.rm_scene_activate(ctx.handle, ctypes.c_void_p(self.raw.data_ptr()),
+                                                 self.num_spheres, ctypes.c_void_p(self._act.data_ptr())),
+                      "rm_scene_activate")
+            self._act_valid = True
         return self._act
 
     def scene(self) -> Scene:
@@ -104,8 +112,9 @@ class Adam:
         p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
         ctx.check(ctx._lib.rm_optimizer_step(ctx.handle, p(self.model.raw), p(grad_act_packed), p(self.m), p(self.v),
                                              self.model.num_spheres, self.t, float(lr), float(self.weight_decay),
-                                             1 if self.with_penalties else 0, p(penalty_out)),
+                                             1 if self.with_penalties else 0, p(penalty_out), p(self.model._act)),
                   "rm_optimizer_step")
+        self.model._act_valid = True
 
 
 # ---- seeded synthetic scenes (BASELINE.md "Synthetic inputs") ------------------------------

@@ -65,10 +65,12 @@ SIGNATURES = {
                                             ctypes.POINTER(RmGrads), _P, _P, _I32]),
     "rm_debug_intermediates": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.POINTER(RmScene),
                                               ctypes.POINTER(RmMarch), _P]),
+    "rm_timing_enable": (ctypes.c_int, [_P, _I32]),
+    "rm_timing_collect": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64), _I32]),
     "rm_scene_activate": (ctypes.c_int, [_P, _P, _I32, _P]),
     "rm_scene_from_packed": (None, [_P, _I32, ctypes.POINTER(RmScene)]),
     "rm_grads_from_packed": (None, [_P, _I32, ctypes.POINTER(RmGrads)]),
-    "rm_optimizer_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _F, _F, _I32, _P]),
+    "rm_optimizer_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _F, _F, _I32, _P, _P]),
 }
 
 _lib = None
@@ -125,6 +127,17 @@ class Context:
         if rc != RM_OK:
             msg = self._lib.rm_last_error(self.handle)
             raise RaymarchError(f"{what} failed with {_ERR_NAMES.get(rc, rc)}: {msg.decode() if msg else ''}")
+
+    def timing(self, enable: bool = True):
+        self.check(self._lib.rm_timing_enable(self.handle, 1 if enable else 0), "rm_timing_enable")
+
+    def collect_timing(self, reset: bool = True):
+        """(summed per-ray kernel milliseconds, launches) since the last reset."""
+        ms = ctypes.c_double()
+        n = _I64()
+        self.check(self._lib.rm_timing_collect(self.handle, ctypes.byref(ms), ctypes.byref(n), 1 if reset else 0),
+                   "rm_timing_collect")
+        return ms.value, n.value
 
     def close(self):
         if getattr(self, "handle", None) is not None and self.handle.value:

@@ -146,6 +146,14 @@ int rm_train_step_camera(rm_context* ctx, const rm_camera* cams, int32_t num_vie
 int rm_debug_intermediates(rm_context* ctx, const float* ray_org, const float* ray_dir, int64_t num_rays,
                            const rm_scene* scene, const rm_march* march, float* dbg);
 
+/* ---- kernel timing (benchmark instrumentation) ------------------------------ */
+/* rm_timing_enable(ctx, 1): every later render / backward / train call records a
+ * hipEvent pair around each launch of its main per-ray kernel on the context's
+ * stream. rm_timing_collect synchronises those events and returns the summed kernel
+ * time in milliseconds and the number of launches (reset != 0 clears the record). */
+int rm_timing_enable(rm_context* ctx, int32_t enable);
+int rm_timing_collect(rm_context* ctx, double* total_ms, int64_t* launches, int32_t reset);
+
 /* ---- model helpers: SceneModel activations, compute_loss penalties, Adam ---- */
 /* Packed parameter layout used by the helpers (raw Param tensors or their grads):
  *   [centers 3M | colors 3M | radius M | light_dir 3 | ambient 1]  (7M+4 floats)
@@ -162,10 +170,12 @@ void rm_grads_from_packed(float* grad_packed, int32_t num_spheres, rm_grads* out
  * coupled L2 weight decay `weight_decay` updates raw_packed in place. adam_m and
  * adam_v are (7M+4)-float device buffers (zero them when re-initialising the
  * optimizer, train.rs:160-163); step counts from 1. loss_penalty (nullable, device
- * float) receives the penalty value. */
+ * float) receives the penalty value at the pre-step parameters. act_out (nullable)
+ * receives the activated packed parameters of the UPDATED model (what
+ * rm_scene_activate would return), so the next render needs no separate launch. */
 int rm_optimizer_step(rm_context* ctx, float* raw_packed, const float* grad_act_packed, float* adam_m,
                       float* adam_v, int32_t num_spheres, int32_t step, float lr, float weight_decay,
-                      int32_t with_penalties, float* loss_penalty);
+                      int32_t with_penalties, float* loss_penalty, float* act_out);
 
 #ifdef __cplusplus
 }

@@ -327,6 +327,10 @@ def test_activation_and_optimizer_match_torch(rm):
         assert abs(host(pen)[0] - pen_loss.item()) < 1e-5 * max(1.0, abs(pen_loss.item()))
         got = host(sm.raw).astype(np.float64)
         assert np.abs(got - theta).max() < 2e-4, np.abs(got - theta).max()
+        # the optimizer's fused activation output == rm_scene_activate of the updated params
+        fused = host(sm._act).copy()
+        sm.invalidate()
+        assert np.array_equal(fused, host(sm.activated_packed()))
         theta = got  # continue from the device state (fp32 rounding)
 
 

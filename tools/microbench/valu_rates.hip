@@ -19,12 +19,14 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
 
-enum Op { OP_FMA, OP_PKFMA, OP_SQRT, OP_EXP, OP_LOG, OP_RCP, OP_MAX, OP_MIX_FMA4_EXP1, OP_MIX_FMA2_EXP1_SQRT1, OP_COUNT };
+enum Op { OP_FMA, OP_PKFMA, OP_SQRT, OP_EXP, OP_LOG, OP_RCP, OP_MAX, OP_MIX_FMA4_EXP1, OP_MIX_FMA2_EXP1_SQRT1,
+          OP_ADD, OP_MAX3, OP_PKADD, OP_RSQ, OP_MAXLIT, OP_COUNT };
 static const char* kNames[OP_COUNT] = {
   "v_fma_f32", "v_pk_fma_f32", "v_sqrt_f32", "v_exp_f32", "v_log_f32", "v_rcp_f32", "v_max_f32",
-  "mix 4 fma + 1 exp", "mix 2 fma + 1 exp + 1 sqrt"};
+  "mix 4 fma + 1 exp", "mix 2 fma + 1 exp + 1 sqrt", "v_add_f32", "v_max3_f32", "v_pk_add_f32", "v_rsq_f32",
+  "v_max_f32 literal"};
 // instructions per chain-step for each op (used to convert to per-instruction rates)
-static const int kInstPerStep[OP_COUNT] = {1, 1, 1, 1, 1, 1, 1, 5, 4};
+static const int kInstPerStep[OP_COUNT] = {1, 1, 1, 1, 1, 1, 1, 5, 4, 1, 1, 1, 1, 1};
 
 template <int OP>
 __global__ __launch_bounds__(256) void bench(float* out, int iters, float seed) {
@@ -61,6 +63,26 @@ __global__ __launch_bounds__(256) void bench(float* out, int iters, float seed) 
 #undef S
     } else if constexpr (OP == OP_MAX) {
 #define S(x) asm volatile("v_max_f32 %0, %0, %1" : "+v"(x) : "v"(c));
+      R8(S)
+#undef S
+    } else if constexpr (OP == OP_ADD) {
+#define S(x) asm volatile("v_add_f32 %0, %0, %1" : "+v"(x) : "v"(c));
+      R8(S)
+#undef S
+    } else if constexpr (OP == OP_MAX3) {
+#define S(x) asm volatile("v_max3_f32 %0, %0, %1, %2" : "+v"(x) : "v"(c), "v"(b));
+      R8(S)
+#undef S
+    } else if constexpr (OP == OP_PKADD) {
+#define S(x) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(x) : "v"(pc));
+      S(p0) S(p1) S(p2) S(p3) S(p0) S(p1) S(p2) S(p3)
+#undef S
+    } else if constexpr (OP == OP_RSQ) {
+#define S(x) asm volatile("v_rsq_f32 %0, %0" : "+v"(x));
+      R8(S)
+#undef S
+    } else if constexpr (OP == OP_MAXLIT) {
+#define S(x) asm volatile("v_max_f32 %0, 0x358637bd, %0" : "+v"(x));
       R8(S)
 #undef S
     } else if constexpr (OP == OP_MIX_FMA4_EXP1) {
@@ -103,22 +125,22 @@ int main() {
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
   const int blocks = cus * 8;  // 8 x 256 threads per CU = 32 waves/CU = 8 waves/SIMD
-  const int iters = 4096;
+  const int iters = 16384;
   double ms[OP_COUNT];
-  ms[OP_FMA] = run<OP_FMA>(d_out, blocks, iters, e0, e1);
-  ms[OP_PKFMA] = run<OP_PKFMA>(d_out, blocks, iters, e0, e1);
-  ms[OP_SQRT] = run<OP_SQRT>(d_out, blocks, iters, e0, e1);
-  ms[OP_EXP] = run<OP_EXP>(d_out, blocks, iters, e0, e1);
-  ms[OP_LOG] = run<OP_LOG>(d_out, blocks, iters, e0, e1);
-  ms[OP_RCP] = run<OP_RCP>(d_out, blocks, iters, e0, e1);
-  ms[OP_MAX] = run<OP_MAX>(d_out, blocks, iters, e0, e1);
-  ms[OP_MIX_FMA4_EXP1] = run<OP_MIX_FMA4_EXP1>(d_out, blocks, iters, e0, e1);
-  ms[OP_MIX_FMA2_EXP1_SQRT1] = run<OP_MIX_FMA2_EXP1_SQRT1>(d_out, blocks, iters, e0, e1);
+  for (int op = 0; op < OP_COUNT; ++op) ms[op] = 1e30;
+  // 5 interleaved rounds; keep the fastest (DVFS and warm-up noise only ever slow a run down)
+  for (int round = 0; round < 5; ++round) {
+    double t;
+#define RUN(OPV) t = run<OPV>(d_out, blocks, iters, e0, e1); if (t < ms[OPV]) ms[OPV] = t;
+    RUN(OP_FMA) RUN(OP_PKFMA) RUN(OP_SQRT) RUN(OP_EXP) RUN(OP_LOG) RUN(OP_RCP) RUN(OP_MAX)
+    RUN(OP_MIX_FMA4_EXP1) RUN(OP_MIX_FMA2_EXP1_SQRT1) RUN(OP_ADD) RUN(OP_MAX3) RUN(OP_PKADD) RUN(OP_RSQ) RUN(OP_MAXLIT)
+#undef RUN
+  }
   printf("%-28s %10s %14s %18s %16s\n", "op", "ms", "lane-op/s", "wave-inst/clk/CU*", "cyc/wave-inst/SIMD*");
   for (int op = 0; op < OP_COUNT; ++op) {
     const double waves = (double)blocks * 4.0;
     const double wave_insts = waves * iters * 8.0 * kInstPerStep[op];
-    const double lane_ops = wave_insts * 64.0 * (op == OP_PKFMA ? 2.0 : 1.0);
+    const double lane_ops = wave_insts * 64.0 * ((op == OP_PKFMA || op == OP_PKADD) ? 2.0 : 1.0);
     const double sec = ms[op] * 1e-3;
     const double per_clk_cu = wave_insts / (sec * clk_ghz * 1e9) / cus;
     printf("%-28s %10.3f %14.4e %18.3f %16.3f\n", kNames[op], ms[op], lane_ops / sec, per_clk_cu,
