@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--ring", type=int, default=10, help="cameras on the target ring")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
-    ap.add_argument("--cpu-sample", type=int, default=8192, help="rays of the CPU baseline sample")
+    ap.add_argument("--cpu-sample", type=int, default=262144, help="rays of the CPU baseline sample")
     return ap.parse_args()
 
 
@@ -166,7 +166,7 @@ def main():
     alg_bytes = rays_per_rank * 12 + blocks * (mpad * 12 + 8) * 4  # target read + partial-gradient slabs
     traffic = None
     traffic_src = None
-    pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")  # committed rocprofv3 PMC summary
     if os.path.exists(pmc_path):
         try:
             pmc = json.load(open(pmc_path))
