@@ -81,6 +81,7 @@ def main():
     from burn_raymarching_amd import model as rmm
     from burn_raymarching_amd import render as rmr
     from burn_raymarching_amd import native
+    from burn_raymarching_amd.parallel import Shard, ViewShardedStep
 
     W, H, M, S, K = args.width, args.height, args.spheres, args.march_steps, args.smooth_k
     vpg = args.views_per_gpu
@@ -103,28 +104,31 @@ def main():
     model = rmm.SceneModel.from_activated(sc0["centers"], sc0["colors"], sc0["radius"], sc0["light_dir"],
                                           sc0["ambient"])
     opt = rmm.Adam(model, weight_decay=1e-5, with_penalties=True)
-    grads = torch.zeros(rmm.packed_size(M), device="cuda")
-    loss = torch.zeros(1, device="cuda")
     tgt_buf = torch.empty((vpg, npix, 3), device="cuda")
     march = native.march_params(S, K)
     ctx = rmr.context()
-    inv_count = 1.0 / (3.0 * rays_global)  # mean over the GLOBAL batch
     total_steps = args.warmup + args.steps
+    progress = {"i": 0}
+
+    def step_fn(views, inv_count, grads_out, loss_out):
+        # rm_train_step_camera over this rank's views (fused forward + loss seed + backward)
+        first = views[0]
+        if views == list(range(first, first + len(views))):
+            tg = targets[first:first + len(views)]
+        else:
+            torch.index_select(targets, 0, torch.tensor(views, device="cuda"), out=tgt_buf)
+            tg = tgt_buf
+        rmr.train_step_camera([cams[j] for j in views], W, H, tg.view(-1, 3), model.scene(), K,
+                              progress=progress["i"] / total_steps, steps=S, inv_count=inv_count,
+                              grads_packed=grads_out, loss=loss_out, march=march)
+
+    dp = ViewShardedStep(Shard(rank, world, vpg, ring), npix, rmm.packed_size(M), "cuda", step_fn,
+                         optim_fn=lambda g: opt.step(g, args.lr))
+    loss = dp.loss
 
     def step(i):
-        first = ((i * world + rank) * vpg) % ring
-        idx = [(first + j) % ring for j in range(vpg)]
-        if idx == list(range(first, first + vpg)):
-            tg = targets[first:first + vpg]
-        else:
-            torch.index_select(targets, 0, torch.tensor(idx, device="cuda"), out=tgt_buf)
-            tg = tgt_buf
-        scene = model.scene()
-        rmr.train_step_camera([cams[j] for j in idx], W, H, tg.view(-1, 3), scene, K, progress=i / total_steps,
-                              steps=S, inv_count=inv_count, grads_packed=grads, loss=loss, march=march)
-        if dist is not None:
-            dist.all_reduce(grads)
-        opt.step(grads, args.lr)
+        progress["i"] = i
+        dp(i)
 
     for i in range(args.warmup):
         step(i)

@@ -1,0 +1,67 @@
+"""View-sharded data parallelism for the training step.
+
+One process per GPU. Rays are independent and every ray does identical work, so whole views
+shard across ranks with perfect balance. The only data-path collective is one sum all-reduce
+of the packed activated-space gradient [centers 3M | colors 3M | radius M | light 3 |
+ambient 1] (7M+4 floats, 28 KB at M=256), plus the 1-float loss: latency-bound messages, so
+RCCL's ring over xGMI is used as is. The loss is normalised by the GLOBAL ray count inside the
+kernel (inv_count = 1/(3 N_global)), so the summed gradient equals the single-process
+gradient of the mean loss. The compute_loss penalties and Adam run replicated AFTER the
+all-reduce (identical on every rank), so they are not multiplied by the world size.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Sequence
+
+import torch
+
+
+@dataclass
+class Shard:
+    rank: int
+    world: int
+    views_per_rank: int
+    ring: int  # number of cameras in the rotation
+
+    def views(self, step: int) -> list[int]:
+        """Views of this rank at `step`: a contiguous block of the ring, rotating every step."""
+        first = ((step * self.world + self.rank) * self.views_per_rank) % self.ring
+        return [(first + j) % self.ring for j in range(self.views_per_rank)]
+
+
+class ViewShardedStep:
+    """One data-parallel training step.
+
+    step_fn(views, inv_count, grads_out, loss_out) computes this rank's contribution (the
+    fused forward + loss seed + backward over its views) into the packed gradient buffer and
+    the loss-sum scalar; the default for training is rm_train_step_camera (see bench.py /
+    train). optim_fn(grads) applies the replicated optimizer step.
+    """
+
+    def __init__(self, shard: Shard, rays_per_view: int, num_params: int, device,
+                 step_fn: Callable[[Sequence[int], float, torch.Tensor, torch.Tensor], None],
+                 optim_fn: Callable[[torch.Tensor], None] | None = None, group=None):
+        self.shard = shard
+        self.rays_global = rays_per_view * shard.views_per_rank * shard.world
+        self.inv_count = 1.0 / (3.0 * self.rays_global)
+        # one buffer, one collective: [packed gradient | loss sum]
+        self.buf = torch.zeros(num_params + 1, device=device)
+        self.grads = self.buf[:num_params]
+        self.loss = self.buf[num_params:]
+        self.step_fn = step_fn
+        self.optim_fn = optim_fn
+        self.group = group
+
+    def __call__(self, step: int) -> None:
+        views = self.shard.views(step)
+        self.step_fn(views, self.inv_count, self.grads, self.loss)
+        if self.shard.world > 1:
+            import torch.distributed as dist
+            dist.all_reduce(self.buf, group=self.group)
+        if self.optim_fn is not None:
+            self.optim_fn(self.grads)
+
+    def mean_loss(self) -> float:
+        """Reconstruction loss (training.rs:34 mean) of the last step, over all ranks."""
+        return float(self.loss.item()) * self.inv_count
