@@ -54,7 +54,8 @@ def parse():
     ap.add_argument("--spheres", type=int, default=256)
     ap.add_argument("--march-steps", type=int, default=32)
     ap.add_argument("--smooth-k", type=float, default=32.0)
-    ap.add_argument("--views-per-gpu", type=int, default=1)
+    ap.add_argument("--views-per-gpu", type=int, default=2,
+                    help="512x512 views per GPU per step (2 amortises the once-per-launch tail)")
     ap.add_argument("--ring", type=int, default=10, help="cameras on the target ring")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")

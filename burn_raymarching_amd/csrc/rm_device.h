@@ -11,7 +11,11 @@
 
 namespace rm {
 
-constexpr int kBlock = 256;              // threads per block = 4 waves
+#ifndef RM_BLOCK
+#define RM_BLOCK 256
+#endif
+constexpr int kBlock = RM_BLOCK;         // threads per block (256 = 4 waves)
+constexpr int kMinWavesPerSimd = 4;      // register budget: <= 128 VGPRs
 constexpr int kWaves = kBlock / 64;
 constexpr int kSphereAlign = 32;         // M is padded to a multiple of this
 constexpr int kChunkBwd = 32;            // spheres per backward partial-combine chunk

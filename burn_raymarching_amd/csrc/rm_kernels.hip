@@ -35,6 +35,10 @@
 #include "../../include/raymarch.h"
 #include "rm_device.h"
 
+#ifndef RM_PRIO_RAMP
+#define RM_PRIO_RAMP 1
+#endif
+
 namespace rm {
 
 enum Mode { kFwd = 0, kBwd = 1, kTrain = 2 };
@@ -275,7 +279,7 @@ __device__ __forceinline__ void shade_sweep(const float p[3], const Lds& L, int 
 
 // ---- the fused per-ray kernel ----------------------------------------------------------
 template <int MODE, bool CAM>
-__global__ __launch_bounds__(kBlock, 4) void rm_ray_kernel(const KArgs a) {
+__global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   Lds L;
   const int tile = a.tile;
@@ -360,7 +364,19 @@ __global__ __launch_bounds__(kBlock, 4) void rm_ray_kernel(const KArgs a) {
   if (MODE == kBwd && a.t_in != nullptr) {
     t = a.t_in[ri];
   } else {
+#if RM_PRIO_RAMP
+    // Equalise progress of the waves sharing a SIMD: VALU issue is arbitrated by priority,
+    // then age, so without this the oldest wave races ahead and the youngest finishes last
+    // (alone, latency-bound) -- a ~14% tail when one launch fills the GPU exactly once.
+    // A wave lowers its priority as it passes checkpoints (march halves, post-march forward,
+    // backward), so laggards win the arbitration.
+    __builtin_amdgcn_s_setprio(3);
+    const int half = max(a.steps / 2, 1);
+#endif
     for (int st = 0; st < a.steps; ++st) {
+#if RM_PRIO_RAMP
+      if (st == half) __builtin_amdgcn_s_setprio(2);
+#endif
       const float p[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
       float m, s;
       const float D = soft_min(p, all_safe(lb), m, s);
@@ -368,6 +384,9 @@ __global__ __launch_bounds__(kBlock, 4) void rm_ray_kernel(const KArgs a) {
       lb = -m * inv_kappa - fabsf(D);
     }
   }
+#if RM_PRIO_RAMP
+  __builtin_amdgcn_s_setprio(1);
+#endif
   if (MODE == kFwd && a.t_out != nullptr && valid) a.t_out[ri] = t;
 
   // ---- reconnect: t_final = t + sdf(p_approx) (renderer_diff.rs:30-39)
@@ -443,6 +462,9 @@ __global__ __launch_bounds__(kBlock, 4) void rm_ray_kernel(const KArgs a) {
     a.out[3 * ri + 2] = outv[2];
   }
   if constexpr (MODE == kFwd) return;
+#if RM_PRIO_RAMP
+  __builtin_amdgcn_s_setprio(0);
+#endif
 
   // ---- seed g = dL/dout
   float g[3] = {0.0f, 0.0f, 0.0f};
@@ -529,12 +551,12 @@ __global__ __launch_bounds__(kBlock, 4) void rm_ray_kernel(const KArgs a) {
           }
         }
         __syncthreads();
-        {
-          const float* s0 = sb + tid;
+        for (int e = tid; e < kChunkBwd * 8; e += kBlock) {
+          const float* s0 = sb + e;
           float acc = s0[0];
 #pragma unroll
           for (int w = 1; w < kWaves; ++w) acc += s0[w * kChunkBwd * 8];
-          rec[(long long)(t0 + jc) * 8 + tid] = acc;
+          rec[(long long)(t0 + jc) * 8 + e] = acc;
         }
       }
     };
@@ -585,12 +607,12 @@ __global__ __launch_bounds__(kBlock, 4) void rm_ray_kernel(const KArgs a) {
           }
         }
         __syncthreads();
-        if (tid < kChunkBwd * 4) {
-          const float* s0 = sb + tid;
+        for (int e = tid; e < kChunkBwd * 4; e += kBlock) {
+          const float* s0 = sb + e;
           float acc = s0[0];
 #pragma unroll
           for (int w = 1; w < kWaves; ++w) acc += s0[w * kChunkBwd * 4];
-          rec[(long long)a.Mpad * 8 + (long long)(t0 + jc) * 4 + tid] = acc;
+          rec[(long long)a.Mpad * 8 + (long long)(t0 + jc) * 4 + e] = acc;
         }
       }
     };

@@ -11,7 +11,7 @@ import os
 import threading
 
 _PKG = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_PKG, "lib", "libraymarch_hip.so")
+LIB_PATH = os.environ.get("RM_LIB_PATH") or os.path.join(_PKG, "lib", "libraymarch_hip.so")
 
 RM_OK = 0
 RM_MAX_VIEWS_PER_CALL = 16
