@@ -41,7 +41,8 @@
 
 namespace rm {
 
-enum Mode { kFwd = 0, kBwd = 1, kTrain = 2 };
+// kRender: the non-differentiable target renderer of renderer.rs:4-80 (generate.rs)
+enum Mode { kFwd = 0, kBwd = 1, kTrain = 2, kRender = 3 };
 
 constexpr int kTileMax = 1024;            // spheres per LDS tile (40 B each)
 constexpr int kMaxBlocksPerLaunch = 4096; // bounds the partial-gradient workspace per launch
@@ -72,6 +73,7 @@ struct KArgs {
   const float* gout;
   const float* targets;
   float progress, inv_count;
+  float light_fixed[3];  // kRender: renderer.rs:27-32 light, normalised on the host in f32
   float* dbg;       // optional per-ray intermediates [n][16] (diagnostics; see rm_debug_intermediates)
   float* partials;  // [gridDim.x][rec], rec = Mpad*12 + 8
   long long rec;
@@ -387,17 +389,17 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
 #if RM_PRIO_RAMP
   __builtin_amdgcn_s_setprio(1);
 #endif
-  if (MODE == kFwd && a.t_out != nullptr && valid) a.t_out[ri] = t;
+  if ((MODE == kFwd || MODE == kRender) && a.t_out != nullptr && valid) a.t_out[ri] = t;
 
-  // ---- reconnect: t_final = t + sdf(p_approx) (renderer_diff.rs:30-39)
+  // ---- reconnect: t_final = t + sdf(p_approx) (renderer_diff.rs:30-39); renderer.rs has none
   const float pa[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
-  float mA, sA;
+  float mA = 0.0f, sA = 1.0f, Da = 0.0f;
   const bool fast_a = all_safe(lb);
-  const float Da = soft_min(pa, fast_a, mA, sA);
+  if constexpr (MODE != kRender) Da = soft_min(pa, fast_a, mA, sA);
   const float tf = t + Da;
   const float p[3] = {fmaf(d[0], tf, o[0]), fmaf(d[1], tf, o[1]), fmaf(d[2], tf, o[2])};
   // p_final is |Da| from p_approx; the taps another eps away
-  const bool fast_f = all_safe(-mA * inv_kappa - fabsf(Da) - a.eps);
+  const bool fast_f = MODE == kRender ? all_safe(lb - a.eps) : all_safe(-mA * inv_kappa - fabsf(Da) - a.eps);
 
   // ---- detached 6-tap normal (scene.rs:81-128)
   float nrm[3];
@@ -423,14 +425,23 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     nrm[2] = nz * inv_len;
   }
 
-  // ---- lighting (renderer_diff.rs:48-62)
-  const float ld0 = a.light_dir[0], ld1 = a.light_dir[1], ld2 = a.light_dir[2];
-  const float amb = a.ambient[0];
-  const float ldlen = sqrtf(ld0 * ld0 + ld1 * ld1 + ld2 * ld2);
-  const float ldn[3] = {ld0 / ldlen, ld1 / ldlen, ld2 / ldlen};
+  // ---- lighting (renderer_diff.rs:48-62; renderer.rs:27-40 in kRender)
+  float ldn[3], amb = 0.0f;
+  if constexpr (MODE == kRender) {
+    ldn[0] = a.light_fixed[0];
+    ldn[1] = a.light_fixed[1];
+    ldn[2] = a.light_fixed[2];
+  } else {
+    const float ld0 = a.light_dir[0], ld1 = a.light_dir[1], ld2 = a.light_dir[2];
+    amb = a.ambient[0];
+    const float ldlen = sqrtf(ld0 * ld0 + ld1 * ld1 + ld2 * ld2);
+    ldn[0] = ld0 / ldlen;
+    ldn[1] = ld1 / ldlen;
+    ldn[2] = ld2 / ldlen;
+  }
   const float sdot = fmaf(nrm[2], ldn[2], fmaf(nrm[1], ldn[1], nrm[0] * ldn[0]));
   const float dif = fmaxf(sdot, 0.0f);
-  const float Lgt = fmaf(dif, 1.0f - amb, amb);
+  const float Lgt = MODE == kRender ? dif + 0.1f : fmaf(dif, 1.0f - amb, amb);
 
   // ---- colour softmax + mask (renderer_diff.rs:64-90)
   const float c10l = a.csharp * kLog2e;
@@ -441,10 +452,25 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   else
     for_tiles([&](int, int tn) { shade_sweep<true>(p, L, tn / 2, c10l, kappa, dmin, Zw2, C2, Zb2); });
   const float Zw = Zw2.x + Zw2.y, Zb = Zb2.x + Zb2.y;
-  const float invZw = frcp(Zw);
-  const float mix[3] = {(C2[0].x + C2[0].y) * invZw, (C2[1].x + C2[1].y) * invZw, (C2[2].x + C2[2].y) * invZw};
   const float Df = dmin - flog2(fmaxf(Zb, 1e-8f)) * inv_kappa;
-  const float mu = frcp(1.0f + fexp2(a.msharp * kLog2e * Df));  // sigmoid(-msharp * D)
+  float mix[3], mu;
+  if constexpr (MODE == kRender) {
+    // renderer.rs:52-71: raw exp(-10 d) weights, mixed = sum(col w) / (sum(w) + 1e-5); the sums
+    // above are shifted by exp(10 dmin), undone here; mask = exp(-10 D^2) (renderer.rs:77)
+    const float e = fexp2(-c10l * dmin);
+    const float den = Zw * e + 1e-5f;
+    mix[0] = (C2[0].x + C2[0].y) * e / den;
+    mix[1] = (C2[1].x + C2[1].y) * e / den;
+    mix[2] = (C2[2].x + C2[2].y) * e / den;
+    mu = fexp2(-10.0f * kLog2e * Df * Df);
+  } else {
+    const float invZw0 = frcp(Zw);
+    mix[0] = (C2[0].x + C2[0].y) * invZw0;
+    mix[1] = (C2[1].x + C2[1].y) * invZw0;
+    mix[2] = (C2[2].x + C2[2].y) * invZw0;
+    mu = frcp(1.0f + fexp2(a.msharp * kLog2e * Df));  // sigmoid(-msharp * D)
+  }
+  const float invZw = frcp(Zw);
   const float scale = Lgt * mu;
   const float outv[3] = {mix[0] * scale, mix[1] * scale, mix[2] * scale};
 
@@ -455,13 +481,13 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
 #pragma unroll
     for (int c = 0; c < 24; ++c) q[c] = vals[c];
   }
-  const bool write_out = (MODE == kFwd || MODE == kTrain) && a.out != nullptr && valid;
+  const bool write_out = MODE != kBwd && a.out != nullptr && valid;
   if (write_out) {
     a.out[3 * ri] = outv[0];
     a.out[3 * ri + 1] = outv[1];
     a.out[3 * ri + 2] = outv[2];
   }
-  if constexpr (MODE == kFwd) return;
+  if constexpr (MODE == kFwd || MODE == kRender) return;
 #if RM_PRIO_RAMP
   __builtin_amdgcn_s_setprio(0);
 #endif
@@ -1003,11 +1029,11 @@ int make_basis(rm_context* ctx, const rm_camera& c, int W, int H, CamBasis& b) {
   return RM_OK;
 }
 
-int check_scene(rm_context* ctx, const rm_scene* s) {
+int check_scene(rm_context* ctx, const rm_scene* s, bool need_light) {
   if (!s) return fail(ctx, RM_ERR_INVALID_ARG, "scene is NULL");
   if (s->num_spheres < 1 || s->num_spheres > RM_MAX_SPHERES)
     return fail(ctx, RM_ERR_INVALID_ARG, "num_spheres %d out of [1, %d]", s->num_spheres, RM_MAX_SPHERES);
-  if (!s->centers || !s->colors || !s->radius || !s->light_dir || !s->ambient)
+  if (!s->centers || !s->colors || !s->radius || (need_light && (!s->light_dir || !s->ambient)))
     return fail(ctx, RM_ERR_INVALID_ARG, "scene has a NULL parameter pointer");
   return RM_OK;
 }
@@ -1054,7 +1080,7 @@ void launch_ray(bool cam, dim3 grid, size_t lds, hipStream_t st, const KArgs& a)
 int run(rm_context* ctx, const Call& c) {
   if (!ctx) return RM_ERR_INVALID_ARG;
   int rc;
-  if ((rc = check_scene(ctx, c.scene)) != RM_OK) return rc;
+  if ((rc = check_scene(ctx, c.scene, c.mode != kRender)) != RM_OK) return rc;
   if ((rc = check_march(ctx, c.march)) != RM_OK) return rc;
   KArgs a;
   std::memset(&a, 0, sizeof a);
@@ -1074,10 +1100,11 @@ int run(rm_context* ctx, const Call& c) {
     if (c.n > 0 && (!c.org || !c.dir)) return fail(ctx, RM_ERR_INVALID_ARG, "ray_org/ray_dir is NULL");
   }
   const long long n = c.cam ? (long long)c.views * c.W * c.H : c.n;
-  if (c.mode == kFwd && n > 0 && !c.out && !c.t_out && !c.dbg) return fail(ctx, RM_ERR_INVALID_ARG, "no output requested");
+  if ((c.mode == kFwd || c.mode == kRender) && n > 0 && !c.out && !c.t_out && !c.dbg) return fail(ctx, RM_ERR_INVALID_ARG, "no output requested");
   if (c.mode == kBwd && n > 0 && !c.gout) return fail(ctx, RM_ERR_INVALID_ARG, "grad_out is NULL");
   if (c.mode == kTrain && n > 0 && !c.targets) return fail(ctx, RM_ERR_INVALID_ARG, "targets is NULL");
-  if (c.mode != kFwd && !c.grads) return fail(ctx, RM_ERR_INVALID_ARG, "grads is NULL");
+  const bool has_bwd = c.mode == kBwd || c.mode == kTrain;
+  if (has_bwd && !c.grads) return fail(ctx, RM_ERR_INVALID_ARG, "grads is NULL");
 
   const int M = c.scene->num_spheres;
   const int Mpad = pad_spheres(M);
@@ -1105,16 +1132,21 @@ int run(rm_context* ctx, const Call& c) {
   a.progress = c.progress;
   a.inv_count = c.inv_count;
   a.dbg = c.dbg;
+  if (c.mode == kRender) {  // renderer.rs:27-32, normalised in f32 on the host like the reference
+    const float lv[3] = {-0.5f, 0.5f, -1.0f};
+    const float len = std::sqrt(lv[0] * lv[0] + lv[1] * lv[1] + lv[2] * lv[2]);
+    for (int i = 0; i < 3; ++i) a.light_fixed[i] = lv[i] / len;
+  }
   a.rec = rec_floats(Mpad);
   const size_t lds = lds_bytes(tile);
 
-  if (c.mode != kFwd) {
+  if (has_bwd) {
     if ((rc = ensure_ws(ctx, ws_need(std::max<long long>(n, 1), M))) != RM_OK) return rc;
   }
   float* P = static_cast<float*>(ctx->ws);
 
   if (n == 0) {  // nothing to render; backward/train still define their outputs
-    if (c.mode == kFwd) return RM_OK;
+    if (!has_bwd) return RM_OK;
   }
   long long done = 0;
   bool first = true;
@@ -1142,11 +1174,12 @@ int run(rm_context* ctx, const Call& c) {
       dim3 grid((unsigned)nb);
       if (c.mode == kFwd) launch_ray<kFwd>(c.cam, grid, lds, ctx->stream, a);
       else if (c.mode == kBwd) launch_ray<kBwd>(c.cam, grid, lds, ctx->stream, a);
-      else launch_ray<kTrain>(c.cam, grid, lds, ctx->stream, a);
+      else if (c.mode == kTrain) launch_ray<kTrain>(c.cam, grid, lds, ctx->stream, a);
+      else launch_ray<kRender>(c.cam, grid, lds, ctx->stream, a);
       RM_HIP(ctx, hipGetLastError());
       if (ev1) RM_HIP(ctx, hipEventRecord(ev1, ctx->stream));
     }
-    if (c.mode != kFwd) {
+    if (has_bwd) {
       const int nblocks = (int)nb;
       const int ncols = Mpad * 8 + 8;
       float* S = P + (long long)std::max<long long>(nb, 1) * a.rec;
@@ -1368,6 +1401,42 @@ int rm_train_step_camera(rm_context* ctx, const rm_camera* cams, int32_t num_vie
   c.loss_sum = loss_sum;
   c.out = out;
   c.accumulate = accumulate;
+  return run(ctx, c);
+}
+
+int rm_render(rm_context* ctx, const float* ray_org, const float* ray_dir, int64_t num_rays, const float* centers,
+              const float* colors, const float* radius, int32_t num_spheres, float* out) {
+  rm_scene sc{centers, colors, radius, nullptr, nullptr, num_spheres};
+  rm_march m;
+  rm_march_default(&m);  // 40 steps, k = 32, eps 1e-4, exp(-10 d) (renderer.rs:17-19, :52)
+  Call c;
+  c.mode = kRender;
+  c.cam = false;
+  c.org = ray_org;
+  c.dir = ray_dir;
+  c.n = num_rays;
+  c.scene = &sc;
+  c.march = &m;
+  c.out = out;
+  return run(ctx, c);
+}
+
+int rm_render_camera(rm_context* ctx, const rm_camera* cams, int32_t num_views, int32_t width, int32_t height,
+                     const float* centers, const float* colors, const float* radius, int32_t num_spheres,
+                     float* out) {
+  rm_scene sc{centers, colors, radius, nullptr, nullptr, num_spheres};
+  rm_march m;
+  rm_march_default(&m);
+  Call c;
+  c.mode = kRender;
+  c.cam = true;
+  c.cams = cams;
+  c.views = num_views;
+  c.W = width;
+  c.H = height;
+  c.scene = &sc;
+  c.march = &m;
+  c.out = out;
   return run(ctx, c);
 }
 

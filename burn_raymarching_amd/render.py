@@ -265,3 +265,35 @@ def create_camera_rays(width, height, eye, target, fov_deg, device="cuda"):
     d = (d / ln).astype(f32).reshape(-1, 3)
     o = np.broadcast_to(eye, d.shape).copy()
     return torch.from_numpy(o).to(device), torch.from_numpy(d).to(device)
+
+
+def render(ray_org, ray_dir, centers, colors, radius):
+    """renderer.rs:4-80 (the non-differentiable target renderer of generate.rs) on the GPU."""
+    n = ray_org.shape[0]
+    m = centers.shape[0]
+    ray_org = _f32(ray_org, (n, 3), "ray_org")
+    ray_dir = _f32(ray_dir, (n, 3), "ray_dir")
+    centers = _f32(centers, (m, 3), "centers")
+    colors = _f32(colors, (m, 3), "colors")
+    radius = _f32(radius.reshape(-1), (m,), "radius")
+    out = torch.empty((n, 3), device=ray_org.device)
+    ctx = context(ray_org.device)
+    ctx.check(ctx._lib.rm_render(ctx.handle, _ptr(ray_org), _ptr(ray_dir), n, _ptr(centers), _ptr(colors),
+                                 _ptr(radius), m, _ptr(out)), "rm_render")
+    return out
+
+
+def render_camera(cams, width, height, centers, colors, radius):
+    """renderer.rs:4-80 with in-kernel camera rays: out [V*H*W, 3] (generate.rs:88-104)."""
+    cams = list(cams)
+    if not 1 <= len(cams) <= native.RM_MAX_VIEWS_PER_CALL:
+        raise ValueError("1..16 views per call")
+    m = centers.shape[0]
+    centers = _f32(centers, (m, 3), "centers")
+    colors = _f32(colors, (m, 3), "colors")
+    radius = _f32(radius.reshape(-1), (m,), "radius")
+    out = torch.empty((len(cams) * width * height, 3), device=centers.device)
+    ctx = context(centers.device)
+    ctx.check(ctx._lib.rm_render_camera(ctx.handle, native.cameras(cams), len(cams), width, height, _ptr(centers),
+                                        _ptr(colors), _ptr(radius), m, _ptr(out)), "rm_render_camera")
+    return out

@@ -138,6 +138,16 @@ int rm_train_step_camera(rm_context* ctx, const rm_camera* cams, int32_t num_vie
                          const rm_scene* scene, const rm_march* march, const rm_grads* grads,
                          float* loss_sum, float* out, int32_t accumulate);
 
+/* ---- non-differentiable target renderer: renderer.rs:4-80 (used by generate.rs) ---- */
+/* 40 march steps at k = 32, detached normal, fixed light (-0.5, 0.5, -1)/|.|, lighting =
+ * diffuse + 0.1, colour = sum(col exp(-10 d)) / (sum(exp(-10 d)) + 1e-5), mask = exp(-10 D^2).
+ * centers/colors/radius are device pointers ([M,3], [M,3], [M]); out [N,3]. */
+int rm_render(rm_context* ctx, const float* ray_org, const float* ray_dir, int64_t num_rays,
+              const float* centers, const float* colors, const float* radius, int32_t num_spheres, float* out);
+int rm_render_camera(rm_context* ctx, const rm_camera* cams, int32_t num_views, int32_t width, int32_t height,
+                     const float* centers, const float* colors, const float* radius, int32_t num_spheres,
+                     float* out);
+
 /* ---- diagnostics ------------------------------------------------------------ */
 /* Per-ray forward intermediates dbg [N][24] = {t, t_final, n.x, n.y, n.z, lighting,
  * mix.r, mix.g, mix.b, D_final, mask, n.l, min delta, Zw, Zb, 0, D(+x), D(-x), D(+y),

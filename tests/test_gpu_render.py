@@ -1,0 +1,85 @@
+"""GPU parity of the non-differentiable target renderer (renderer.rs:4-80, used by generate.rs)
+through the C ABI (rm_render / rm_render_camera): the reference's own data/target_*.png KAT
+on the GPU path, plus the f32 oracle on random scenes."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import DANGO, GOLDEN, gpu_available, load_png
+
+pytestmark = pytest.mark.gpu
+
+# the same budget as the render_diff forward parity (test_gpu_parity.py)
+FWD_MAX = 1e-3
+FWD_MEAN = 1e-5
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not gpu_available():
+        pytest.skip("no GPU")
+    import torch
+    return torch.device("cuda:0")
+
+
+def _dango(dev):
+    import torch
+    return [torch.tensor(DANGO[k], device=dev) for k in ("centers", "colors", "radius")]
+
+
+def test_render_camera_matches_target_pngs(dev, oracle):
+    """All ten data/target_i.png (generate.rs:88-104) from one 10-view GPU launch, +-1 LSB."""
+    from burn_raymarching_amd import render as R
+    cams = json.load(open(os.path.join(GOLDEN, "cameras.json")))
+    views = [(c["origin"], c["target"], c["fov"]) for c in cams]
+    out = R.render_camera(views, 256, 256, *_dango(dev)).cpu().numpy().reshape(len(views), 256, 256, 3)
+    for v in range(len(views)):
+        png = oracle.to_png_bytes(out[v]).astype(int)
+        ref = load_png(os.path.join(GOLDEN, "target_%d.png" % v)).astype(int)
+        diff = np.abs(png - ref)
+        assert diff.max() <= 1, (v, diff.max())
+        assert (diff > 0).sum() <= 64, (v, (diff > 0).sum())
+
+
+def test_render_array_equals_camera(dev, oracle):
+    """Array-mode rays from create_camera_rays give the same image bit for bit."""
+    import torch
+    from burn_raymarching_amd import render as R
+    cams = json.load(open(os.path.join(GOLDEN, "cameras.json")))
+    c = cams[3]
+    o, d = R.create_camera_rays(96, 64, c["origin"], c["target"], c["fov"], device=dev)
+    a = R.render(o, d, *_dango(dev))
+    o, d = o.cpu().numpy(), d.cpu().numpy()
+    b = R.render_camera([(c["origin"], c["target"], c["fov"])], 96, 64, *_dango(dev))
+    assert torch.equal(a, b)
+    ref = oracle.render(o, d, DANGO["centers"], DANGO["colors"], DANGO["radius"])
+    err = np.abs(a.cpu().numpy() - ref)
+    assert err.max() < FWD_MAX and err.mean() < FWD_MEAN
+
+
+@pytest.mark.parametrize("M,seed", [(8, 0), (64, 1), (300, 2), (1100, 3)])
+def test_render_random_scene_vs_oracle(dev, oracle, M, seed):
+    """Random scenes (multi-tile at M=1100) against the f32 oracle restatement of renderer.rs."""
+    import torch
+    from burn_raymarching_amd import model as Mdl, render as R
+    sc = Mdl.synthetic_scene(M, seed)
+    og, dg = R.create_camera_rays(48, 40, [0.3, 0.4, -2.5], [0.0, 0.0, 0.0], 50.0, device=dev)
+    t = lambda x: torch.tensor(np.asarray(x, np.float32), device=dev)
+    out = R.render(og, dg, t(sc["centers"]), t(sc["colors"]), t(sc["radius"])).cpu().numpy()
+    o, d = og.cpu().numpy(), dg.cpu().numpy()
+    ref = oracle.render(o, d, sc["centers"], sc["colors"], sc["radius"])
+    err = np.abs(out - ref)
+    assert np.isfinite(out).all()
+    assert err.max() < FWD_MAX and err.mean() < FWD_MEAN, (err.max(), err.mean())
+
+
+def test_render_invalid_args(dev):
+    import torch
+    from burn_raymarching_amd import render as R
+    c, col, r = _dango(dev)
+    with pytest.raises(ValueError):
+        R.render_camera([], 8, 8, c, col, r)
+    o = torch.zeros((0, 3), device=dev)
+    assert R.render(o, o, c, col, r).shape == (0, 3)
