@@ -1,7 +1,8 @@
 """Build recipe for the in-tree native libraries (hipcc for gfx950; no JIT cache).
 
   burn_raymarching_amd/lib/libraymarch_hip.so  <- csrc/rm_kernels.hip   (the product: C ABI of include/raymarch.h)
-  burn_raymarching_amd/lib/rm_train             <- csrc/host/*.cpp       (C++ host: Scene/Camera/train loop)
+  burn_raymarching_amd/lib/librm_host.so        <- csrc/host/{io,data,driver}.cpp (C ABI of include/rm_host.h)
+  burn_raymarching_amd/lib/rm_train             <- csrc/host/main.cpp    (CLI: train / generate / preview)
 
 Run ``python -m burn_raymarching_amd._build`` or ``__graft_entry__.build()``.
 """
@@ -18,6 +19,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIBDIR = os.path.join(PKG, "lib")
 ARCH = os.environ.get("RM_OFFLOAD_ARCH", "gfx950")
 LIB = os.path.join(LIBDIR, "libraymarch_hip.so")
+HOST_LIB = os.path.join(LIBDIR, "librm_host.so")
 
 
 def _hipcc() -> str:
@@ -48,17 +50,29 @@ def build_lib(force: bool = False, verbose: bool = False) -> str:
 
 
 def build_host(force: bool = False, verbose: bool = False) -> str:
-    """C++ host (train loop) linked against libraymarch_hip.so."""
+    """librm_host.so (include/rm_host.h: files, dataset, prune_and_split, train driver) and the
+    rm_train CLI, both C++ host code linked against libraymarch_hip.so."""
     host_dir = os.path.join(CSRC, "host")
     if not os.path.isdir(host_dir):
         return ""
     lib = build_lib(force=force, verbose=verbose)
+    inc = os.path.join(ROOT, "include")
+    headers = [os.path.join(inc, "raymarch.h"), os.path.join(inc, "rm_host.h"),
+               os.path.join(host_dir, "rmh_common.hpp")]
+    lib_srcs = [os.path.join(host_dir, f) for f in ("io.cpp", "data.cpp", "driver.cpp")]
+    # -ffp-contract=off: the host f32 arithmetic (camera rays, prune_and_split) keeps the
+    # reference's rounding, no fused multiply-adds
+    common = [_hipcc(), "-O2", "-std=c++17", "-Wall", "-fPIC", "-ffp-contract=off", "-I", inc]
+    rpath = ["-Wl,-rpath,$ORIGIN"]
+    if force or _stale(HOST_LIB, lib_srcs + headers + [lib]):
+        cmd = common + ["-shared", "-o", HOST_LIB] + lib_srcs + ["-L", LIBDIR, "-lraymarch_hip", "-lz"] + rpath
+        if verbose:
+            print(" ".join(cmd), file=sys.stderr)
+        subprocess.run(cmd, check=True)
     exe = os.path.join(LIBDIR, "rm_train")
-    srcs = sorted(os.path.join(host_dir, f) for f in os.listdir(host_dir) if f.endswith((".cpp", ".hpp")))
-    cpp = [s for s in srcs if s.endswith(".cpp")]
-    if force or _stale(exe, srcs + [lib, os.path.join(ROOT, "include", "raymarch.h")]):
-        cmd = [_hipcc(), "-O2", "-std=c++17", "-Wall", "-I", os.path.join(ROOT, "include"), "-o", exe] + cpp + [
-            "-L", LIBDIR, "-lraymarch_hip", f"-Wl,-rpath,{LIBDIR}", "-Wl,-rpath,$ORIGIN", "-lz"]
+    main = os.path.join(host_dir, "main.cpp")
+    if force or _stale(exe, [main, HOST_LIB] + headers):
+        cmd = common + ["-o", exe, main, "-L", LIBDIR, "-lrm_host", "-lraymarch_hip"] + rpath
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)

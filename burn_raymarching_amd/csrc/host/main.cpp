@@ -1,0 +1,125 @@
+// rm_train: command-line front end of librm_host.so, standing in for the reference's
+// binaries (src/bin/train.rs, src/bin/generate.rs) on MI355X.
+//
+//   rm_train train    [--cameras data/cameras.json] [--out .] [--stages 5] [--steps 700]
+//                     [--batch 16384] [--size 256x256] [--march-steps 40] [--seed 0]
+//                     [--log-every 100] [--no-previews] [--device 0]
+//   rm_train generate [--out data] [--prefix data/] [--size 256x256] [--device 0]
+//   rm_train preview  --scene scene.json --png out.png [--size 256x256]
+//                     [--eye 0,0,-2.5] [--target 0,0,0] [--fov 50] [--radius-offset 0.01]
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+
+#include "rm_host.h"
+
+namespace {
+
+int usage() {
+  std::fprintf(stderr,
+               "usage: rm_train train|generate|preview [options]\n"
+               "  train    --cameras F --out D --stages N --steps N --batch N --size WxH --march-steps N\n"
+               "           --seed N --log-every N --no-previews --device N\n"
+               "  generate --out D --prefix P --size WxH --device N\n"
+               "  preview  --scene F --png F --size WxH --eye x,y,z --target x,y,z --fov F --radius-offset F\n");
+  return 2;
+}
+
+bool parse_size(const char* s, int32_t& w, int32_t& h) { return std::sscanf(s, "%dx%d", &w, &h) == 2 && w > 0 && h > 0; }
+
+bool parse_vec3(const char* s, float v[3]) { return std::sscanf(s, "%f,%f,%f", &v[0], &v[1], &v[2]) == 3; }
+
+int report(int rc, const char* what) {
+  if (rc != RMH_OK) std::fprintf(stderr, "rm_train %s: %s\n", what, rmh_last_error());
+  return rc == RMH_OK ? 0 : 1;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 2) return usage();
+  const std::string cmd = argv[1];
+  auto need = [&](int i) { return i + 1 < argc; };
+  if (cmd == "train") {
+    rmh_train_config cfg;
+    rmh_train_config_default(&cfg);
+    for (int i = 2; i < argc; ++i) {
+      const std::string a = argv[i];
+      if (a == "--no-previews") {
+        cfg.previews = 0;
+      } else if (!need(i)) {
+        return usage();
+      } else if (a == "--cameras") {
+        cfg.cameras_json = argv[++i];
+      } else if (a == "--out") {
+        cfg.out_dir = argv[++i];
+      } else if (a == "--stages") {
+        cfg.stages = std::atoi(argv[++i]);
+      } else if (a == "--steps") {
+        cfg.steps_per_stage = std::atoi(argv[++i]);
+      } else if (a == "--batch") {
+        cfg.batch = std::atoi(argv[++i]);
+      } else if (a == "--size") {
+        if (!parse_size(argv[++i], cfg.width, cfg.height)) return usage();
+      } else if (a == "--march-steps") {
+        cfg.march_steps = std::atoi(argv[++i]);
+      } else if (a == "--seed") {
+        cfg.seed = std::strtoull(argv[++i], nullptr, 10);
+      } else if (a == "--log-every") {
+        cfg.log_every = std::atoi(argv[++i]);
+      } else if (a == "--device") {
+        cfg.device = std::atoi(argv[++i]);
+      } else {
+        return usage();
+      }
+    }
+    rmh_train_result res;
+    const int rc = rmh_train(&cfg, &res, nullptr, 0);
+    if (rc == RMH_OK)
+      std::printf("{\"num_spheres\": %d, \"steps\": %d, \"final_loss\": %.6g, \"seconds\": %.4f, \"step_ms\": %.4f}\n",
+                  res.num_spheres, res.steps, res.final_loss, res.seconds, res.step_ms);
+    return report(rc, "train");
+  }
+  if (cmd == "generate") {
+    const char* out = "data";
+    const char* prefix = "data/";
+    int32_t w = 256, h = 256, dev = 0;
+    for (int i = 2; i < argc; ++i) {
+      const std::string a = argv[i];
+      if (!need(i)) return usage();
+      if (a == "--out") out = argv[++i];
+      else if (a == "--prefix") prefix = argv[++i];
+      else if (a == "--size") {
+        if (!parse_size(argv[++i], w, h)) return usage();
+      } else if (a == "--device") dev = std::atoi(argv[++i]);
+      else return usage();
+    }
+    return report(rmh_generate(out, prefix, w, h, dev), "generate");
+  }
+  if (cmd == "preview") {
+    const char* scene = nullptr;
+    const char* png = nullptr;
+    int32_t w = 256, h = 256, dev = 0;
+    float eye[3] = {0.0f, 0.0f, -2.5f}, tgt[3] = {0.0f, 0.0f, 0.0f}, fov = 50.0f, roff = 0.01f;
+    for (int i = 2; i < argc; ++i) {
+      const std::string a = argv[i];
+      if (!need(i)) return usage();
+      if (a == "--scene") scene = argv[++i];
+      else if (a == "--png") png = argv[++i];
+      else if (a == "--size") {
+        if (!parse_size(argv[++i], w, h)) return usage();
+      } else if (a == "--eye") {
+        if (!parse_vec3(argv[++i], eye)) return usage();
+      } else if (a == "--target") {
+        if (!parse_vec3(argv[++i], tgt)) return usage();
+      } else if (a == "--fov") fov = (float)std::atof(argv[++i]);
+      else if (a == "--radius-offset") roff = (float)std::atof(argv[++i]);
+      else if (a == "--device") dev = std::atoi(argv[++i]);
+      else return usage();
+    }
+    if (!scene || !png) return usage();
+    return report(rmh_preview(scene, png, w, h, eye, tgt, fov, roff, dev), "preview");
+  }
+  return usage();
+}

@@ -783,6 +783,25 @@ __device__ __forceinline__ float activate_elem(float x, int i, int M) {
   return sigmoidf_(x);                               // ambient = sigmoid(raw)       scene.rs:45
 }
 
+// dataset.rs:75-79: rows idx[i] of the ray / target arrays -> the batch (3 floats per row per
+// array). An index outside [0, num_src) yields a zero row rather than an out-of-bounds read.
+__global__ __launch_bounds__(256) void rm_gather_kernel(const float* __restrict__ org, const float* __restrict__ dir,
+                                                        const float* __restrict__ tgt, long long num_src,
+                                                        const int32_t* __restrict__ idx, long long n,
+                                                        float* __restrict__ oo, float* __restrict__ od,
+                                                        float* __restrict__ ot) {
+  const long long e = (long long)blockIdx.x * 256 + threadIdx.x;  // one float of the [n,3] batch
+  if (e >= 3 * n) return;
+  const long long i = e / 3;
+  const int c = (int)(e - 3 * i);
+  const long long j = idx[i];
+  const bool ok = j >= 0 && j < num_src;
+  const long long s = 3 * j + c;
+  if (oo) oo[e] = ok ? org[s] : 0.0f;
+  if (od) od[e] = ok ? dir[s] : 0.0f;
+  if (ot) ot[e] = ok ? tgt[s] : 0.0f;
+}
+
 __global__ __launch_bounds__(256) void rm_activate_kernel(const float* __restrict__ raw, int M,
                                                           float* __restrict__ act) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -1462,6 +1481,24 @@ int rm_scene_activate(rm_context* ctx, const float* raw_packed, int32_t num_sphe
   const int n = 7 * num_spheres + 4;
   hipLaunchKernelGGL(rm::rm_activate_kernel, dim3((n + 255) / 256), dim3(256), 0, ctx->stream, raw_packed,
                      num_spheres, act_packed);
+  RM_HIP(ctx, hipGetLastError());
+  return RM_OK;
+}
+
+int rm_gather_rays(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
+                   int64_t num_src, const int32_t* indices, int64_t num_rays, float* out_org, float* out_dir,
+                   float* out_targets) {
+  if (!ctx) return RM_ERR_INVALID_ARG;
+  if (num_rays < 0 || num_src < 0) return fail(ctx, RM_ERR_INVALID_ARG, "negative size");
+  if (num_rays == 0) return RM_OK;
+  if (!indices) return fail(ctx, RM_ERR_INVALID_ARG, "indices is NULL");
+  if ((out_org && !ray_org) || (out_dir && !ray_dir) || (out_targets && !targets))
+    return fail(ctx, RM_ERR_INVALID_ARG, "an output is requested without its source array");
+  if (!out_org && !out_dir && !out_targets) return fail(ctx, RM_ERR_INVALID_ARG, "no output requested");
+  const long long nel = 3 * (long long)num_rays;
+  hipLaunchKernelGGL(rm::rm_gather_kernel, dim3((unsigned)((nel + 255) / 256)), dim3(256), 0, ctx->stream, ray_org,
+                     ray_dir, targets, (long long)num_src, indices, (long long)num_rays, out_org, out_dir,
+                     out_targets);
   RM_HIP(ctx, hipGetLastError());
   return RM_OK;
 }

@@ -65,6 +65,7 @@ SIGNATURES = {
                                             ctypes.POINTER(RmGrads), _P, _P, _I32]),
     "rm_render": (ctypes.c_int, [_P, _P, _P, _I64, _P, _P, _P, _I32, _P]),
     "rm_render_camera": (ctypes.c_int, [_P, ctypes.POINTER(RmCamera), _I32, _I32, _I32, _P, _P, _P, _I32, _P]),
+    "rm_gather_rays": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _P, _P, _P]),
     "rm_debug_intermediates": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.POINTER(RmScene),
                                               ctypes.POINTER(RmMarch), _P]),
     "rm_timing_enable": (ctypes.c_int, [_P, _I32]),

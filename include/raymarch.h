@@ -148,6 +148,14 @@ int rm_render_camera(rm_context* ctx, const rm_camera* cams, int32_t num_views, 
                      const float* centers, const float* colors, const float* radius, int32_t num_spheres,
                      float* out);
 
+/* ---- batch gather: SceneDataset::sample_batch, dataset.rs:75-79 ---------------- */
+/* out_*[i] = src[indices[i]] for the ray origin, direction and target arrays ([num_src,3]
+ * each; any output may be NULL to skip it). indices is a device int32 [num_rays]; an index
+ * outside [0, num_src) gives a zero row. */
+int rm_gather_rays(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
+                   int64_t num_src, const int32_t* indices, int64_t num_rays, float* out_org, float* out_dir,
+                   float* out_targets);
+
 /* ---- diagnostics ------------------------------------------------------------ */
 /* Per-ray forward intermediates dbg [N][24] = {t, t_final, n.x, n.y, n.z, lighting,
  * mix.r, mix.g, mix.b, D_final, mask, n.l, min delta, Zw, Zb, 0, D(+x), D(-x), D(+y),

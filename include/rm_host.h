@@ -1,0 +1,158 @@
+/*
+ * rm_host.h -- C ABI of librm_host.so: the host side of the reference's training and
+ * target-generation programs, rebuilt in C++ over libraymarch_hip.so (include/raymarch.h).
+ *
+ * The reference's host code is Rust (no toolchain in this image); these entry points are
+ * what its binaries do around the hot path:
+ *   - util.rs:4-33          PNG save/load with the 2.2 gamma            -> rmh_image_*, rmh_png_*
+ *   - camera.rs:30-90       create_camera_rays (host f32 loop)          -> rmh_camera_rays
+ *   - train.rs:15-21, generate.rs:13-18, :107-109   cameras.json        -> rmh_cameras_*
+ *   - train.rs:210-262      scene.json export                           -> rmh_scene_*
+ *   - dataset.rs:4-82       SceneDataset fg/bg split + sample_batch     -> rmh_dataset_*
+ *   - training.rs:87-238    prune_and_split                             -> rmh_prune_and_split
+ *   - train.rs:23-330       the multi-stage training driver             -> rmh_train
+ *   - train.rs:335-366      save_tiled_preview                          -> rmh_preview
+ *   - generate.rs:20-112    the synthetic target generator              -> rmh_generate
+ *
+ * Everything except rmh_train / rmh_preview / rmh_generate is CPU-only. The reference's RNG
+ * is unseeded (rand::rng(), dataset.rs:52, training.rs:93); here every random draw comes from
+ * an explicit, seeded PCG32 stream (rmh_rng) so runs are reproducible.
+ *
+ * Return values: RMH_OK (0) or an RMH_ERR_* code; rmh_last_error() has the text (per thread).
+ * Buffers returned through `**` out-parameters are malloc'd; release them with rmh_free().
+ */
+#ifndef RM_HOST_H_
+#define RM_HOST_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RMH_OK 0
+#define RMH_ERR_INVALID_ARG 1
+#define RMH_ERR_IO 2
+#define RMH_ERR_FORMAT 3
+#define RMH_ERR_GPU 4
+
+const char* rmh_last_error(void);
+void rmh_free(void* p);
+
+/* ---- util.rs: images ----------------------------------------------------------------- */
+/* 8-bit PNG (grey, grey+alpha, RGB, RGBA, palette; non-interlaced) -> RGB8 [h][w][3]. */
+int rmh_png_read(const char* path, int32_t* width, int32_t* height, uint8_t** rgb);
+/* RGB8 -> PNG; creates missing parent directories (util.rs:14-18). */
+int rmh_png_write(const char* path, const uint8_t* rgb, int32_t width, int32_t height);
+/* util.rs:28-31: (x / 255) ^ 2.2 in f32. */
+void rmh_srgb8_to_linear(const uint8_t* in, int64_t n, float* out);
+/* util.rs:6-9: (x ^ (1/2.2)).clamp(0, 1) * 255 truncated to u8 (NaN -> 0). */
+void rmh_linear_to_srgb8(const float* in, int64_t n, uint8_t* out);
+/* load_image_as_tensor (util.rs:24-33): linear RGB [h*w][3]. */
+int rmh_image_load(const char* path, int32_t* width, int32_t* height, float** linear_rgb);
+/* save_tensor_as_image (util.rs:4-21) of a HOST buffer [h*w][3]. */
+int rmh_image_save(const char* path, const float* linear_rgb, int32_t width, int32_t height);
+
+/* ---- camera.rs:30-90 ----------------------------------------------------------------- */
+/* org, dir: host [height*width][3], rows y then x (no half-pixel offset). */
+void rmh_camera_rays(int32_t width, int32_t height, const float eye[3], const float target[3], float fov_deg,
+                     float* org, float* dir);
+
+/* ---- cameras.json: Vec<CameraConfig{file, origin, target, fov}> --------------------- */
+#define RMH_PATH_MAX 512
+typedef struct rmh_camera_entry {
+  char file[RMH_PATH_MAX];
+  float origin[3];
+  float target[3];
+  float fov;
+} rmh_camera_entry;
+int rmh_cameras_load(const char* path, rmh_camera_entry** cams, int32_t* count);
+/* serde_json::to_writer_pretty layout (generate.rs:107-109). */
+int rmh_cameras_save(const char* path, const rmh_camera_entry* cams, int32_t count);
+
+/* ---- scene.json (train.rs:238-262): activated values, radius WITHOUT the +0.01 -------- */
+int rmh_scene_save(const char* path, int32_t num_spheres, const float* centers, const float* colors,
+                   const float* radii, const float* light_dir, const float* ambient);
+int rmh_scene_load(const char* path, int32_t* num_spheres, float** centers, float** colors, float** radii,
+                   float light_dir[3], float* ambient);
+
+/* ---- seeded RNG (PCG32, O'Neill 2014) ------------------------------------------------ */
+typedef struct rmh_rng {
+  uint64_t state;
+  uint64_t inc;
+} rmh_rng;
+void rmh_rng_seed(rmh_rng* rng, uint64_t seed, uint64_t stream);
+uint32_t rmh_rng_u32(rmh_rng* rng);
+/* Uniform integer in [0, n) (Lemire's unbiased bounded method); n >= 1. */
+uint32_t rmh_rng_below(rmh_rng* rng, uint32_t n);
+/* Uniform float in [lo, hi) with 24 random bits. */
+float rmh_rng_uniform(rmh_rng* rng, float lo, float hi);
+
+/* ---- dataset.rs: SceneDataset --------------------------------------------------------- */
+typedef struct rmh_dataset rmh_dataset;
+/* targets: host linear RGB [num_pixels][3]; fg = pixels with R+G+B > 0.05 (dataset.rs:26-35). */
+int rmh_dataset_create(const float* targets, int64_t num_pixels, rmh_dataset** out);
+void rmh_dataset_destroy(rmh_dataset* ds);
+void rmh_dataset_counts(const rmh_dataset* ds, int64_t* num_fg, int64_t* num_bg);
+/* sample_batch index draw (dataset.rs:47-73): floor(batch*ratio) uniform pixels, then the
+ * rest uniformly from the foreground list (shrunk to |fg| when fg is smaller). *count gets
+ * the number written: like the reference, a dataset without foreground gives a short batch. */
+int rmh_dataset_sample(const rmh_dataset* ds, int32_t batch, float uniform_ratio, rmh_rng* rng, int32_t* indices,
+                       int32_t* count);
+
+/* ---- training.rs:87-238: prune_and_split ---------------------------------------------- */
+/* raw_packed: the model's RAW params [centers 3M | colors 3M | radius M | light 3 | ambient 1];
+ * init_centers [M][3]: the centres the stage started from. out_packed (capacity 14M+4 floats)
+ * receives the next generation in the same layout, light/ambient carried over; out_M its M.
+ * Returns RMH_ERR_INVALID_ARG if every sphere was pruned. */
+int rmh_prune_and_split(const float* raw_packed, int32_t num_spheres, const float* init_centers, int32_t stage,
+                        int32_t stages, rmh_rng* rng, float* out_packed, int32_t* out_num_spheres);
+/* The initial 7-sphere raw model of train.rs:100-126 (out: 7*7+4 floats). */
+void rmh_initial_model(float* raw_packed);
+
+/* ---- train.rs: the driver ------------------------------------------------------------- */
+typedef struct rmh_train_config {
+  const char* cameras_json; /* data/cameras.json; image paths resolved against its directory */
+  const char* out_dir;      /* scene.json and steps/ previews go here (NULL: no output files) */
+  int32_t width, height;    /* 256 x 256 (train.rs:32-33) */
+  int32_t stages;           /* 5 (train.rs:128) */
+  int32_t steps_per_stage;  /* 700 (train.rs:129) */
+  int32_t batch;            /* 16384 (train.rs:30) */
+  int32_t march_steps;      /* 40 (renderer_diff.rs:22) */
+  float max_smooth;         /* 32 (train.rs:131) */
+  float base_lr;            /* 0.05 (train.rs:166) */
+  float weight_decay;       /* 1e-5 (train.rs:161) */
+  int32_t log_every;        /* 100 (train.rs:200); 0 = silent */
+  int32_t previews;         /* write steps/stage_i.png and steps/final_1.png */
+  uint64_t seed;
+  int32_t device;
+} rmh_train_config;
+void rmh_train_config_default(rmh_train_config* cfg);
+
+typedef struct rmh_train_result {
+  int32_t num_spheres;   /* M of the exported model */
+  int32_t steps;         /* optimizer steps taken */
+  float final_loss;      /* compute_loss of the last step */
+  double seconds;        /* wall time of the stage loops (GPU synchronised) */
+  double step_ms;        /* mean per-step time (sample + gather + train step + optimizer) */
+} rmh_train_result;
+/* raw_out (nullable, capacity 7*M_max+4) receives the final RAW packed params. */
+int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_out, int32_t raw_capacity);
+
+/* ---- train.rs:335-366: preview of a scene.json (render_diff, S=40, k=32) --------------- */
+/* radius_offset: 0.01 reproduces the model's activation (scene.rs:43); scene.json stores
+ * softplus(raw) without it. */
+int rmh_preview(const char* scene_json, const char* png_path, int32_t width, int32_t height, const float eye[3],
+                const float target[3], float fov_deg, float radius_offset, int32_t device);
+
+/* ---- generate.rs:20-112: target images + cameras.json ---------------------------------- */
+/* Renders the three-sphere scene from the 10 generate.rs cameras with rm_render_camera and
+ * writes out_dir/target_i.png plus out_dir/cameras.json ("file" entries are
+ * "<file_prefix>target_i.png"; generate.rs uses "data/"). */
+int rmh_generate(const char* out_dir, const char* file_prefix, int32_t width, int32_t height, int32_t device);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RM_HOST_H_ */
