@@ -1,0 +1,56 @@
+"""The build's C1 golden vectors (made by tools/make_golden.py from the
+oracle): the oracle still reproduces them (CPU), and the GPU path matches the fp64 values
+(GPU, same tolerances as tests/test_gpu_parity.py)."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, gpu_available
+
+FILES = sorted(glob.glob(os.path.join(GOLDEN, "c1_S*_k*.npz")))
+KEYS = ("centers", "radius", "colors", "light_dir", "ambient")
+
+
+def _scene(z):
+    return {k: z["scene_" + k] for k in KEYS}
+
+
+def test_golden_files_present():
+    assert len(FILES) == 4
+
+
+@pytest.mark.parametrize("path", FILES, ids=os.path.basename)
+def test_oracle_reproduces_golden(oracle, path):
+    z = np.load(path)
+    steps, k = int(z["steps"]), float(z["smooth_k"])
+    o, d = z["ray_org"], z["ray_dir"]
+    for prec, dt, rtol in (("f64", np.float64, 1e-10), ("f32", np.float32, 2e-4)):
+        out = oracle.render_diff(o, d, _scene(z), steps, k, precision=prec)
+        assert np.array_equal(out, z[f"out_{prec}"])  # per-ray work is deterministic
+        gr = oracle.render_diff_backward(o, d, _scene(z), steps, k, z["grad_out"].astype(dt), precision=prec)
+        for key in KEYS:
+            ref = z[f"grad_{key}_{prec}"]
+            assert np.allclose(gr[key], ref, rtol=rtol, atol=rtol * np.abs(ref).max()), (prec, key)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")
+@pytest.mark.parametrize("path", FILES, ids=os.path.basename)
+def test_gpu_matches_golden(path):
+    import torch
+    from burn_raymarching_amd import render
+    from test_gpu_parity import FWD_MAX, FWD_MEAN, GRAD_TOL
+    z = np.load(path)
+    steps, k = int(z["steps"]), float(z["smooth_k"])
+    dv = lambda x: torch.from_numpy(np.ascontiguousarray(x, np.float32)).cuda()
+    sc = render.Scene(*(dv(z["scene_" + key]) for key in ("centers", "colors", "radius", "light_dir", "ambient")))
+    out = render.render_diff_forward(dv(z["ray_org"]), dv(z["ray_dir"]), sc, k, steps).cpu().numpy()
+    e = np.abs(out - z["out_f64"])
+    assert e.max() <= FWD_MAX and e.mean() <= FWD_MEAN, (e.max(), e.mean())
+    gr = render.render_diff_backward(dv(z["ray_org"]), dv(z["ray_dir"]), sc, k, dv(z["grad_out"]), steps)
+    for key, tol in GRAD_TOL.items():
+        ref = z[f"grad_{key}_f64"].reshape(-1)
+        err = np.abs(gr[key].cpu().numpy().reshape(-1) - ref).max()
+        assert err <= tol * np.abs(ref).max(), (key, err)
