@@ -12,13 +12,18 @@ HIP path, per rank:
 Views shard across ranks (weak scaling: every rank renders its own 512x512 view per step).
 value = rays of all ranks / max-over-ranks wall time of the K timed steps.
 
+--skip-escaped on (off by default, like the library): ray blocks whose rays provably leave the
+scene with a silhouette mask of exactly 0 get out = 0 and zero gradients without marching --
+bit-identical results (tests/test_gpu_escape.py); `escape_skip` reports the skipped share.
+
 Synthetic data (no datasets offline): scene seed 0 (BASELINE.md "Synthetic inputs"), targets
 = the seed-1 scene rendered by the forward kernel from a ring of cameras at radius 2.5, y 0.5.
 
 Extra objects on the JSON line:
   roofline      -- the dominant kernel (rm_ray_kernel<train>) timed with hipEvents on its own
                    stream inside the timed region; algorithmic FLOP = 16*(S+10)*M per ray
-                   (SURVEY.md §8d); bound "valu" (fp32 vector; no MFMA/HBM-bound work here);
+                    for the rays whose sphere work actually ran (blocks skipped
+                   by the exact escape test count zero); bound "valu" (fp32 vector);
                    traffic = HBM bytes per launch from the committed rocprofv3 PMC summary
                    (profiles/r01_pmc_traffic.json) when present, else null.
   cpu_baseline  -- the oracle's fp32 reference-order C restatement (OpenMP) on a bounded
@@ -60,6 +65,8 @@ def parse():
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-sample", type=int, default=262144, help="rays of the CPU baseline sample")
+    ap.add_argument("--skip-escaped", choices=["on", "off"], default="off",
+                    help="RM_MARCH_SKIP_ESCAPED: skip ray blocks that provably leave the scene (exact)")
     return ap.parse_args()
 
 
@@ -106,7 +113,7 @@ def main():
                                           sc0["ambient"])
     opt = rmm.Adam(model, weight_decay=1e-5, with_penalties=True)
     tgt_buf = torch.empty((vpg, npix, 3), device="cuda")
-    march = native.march_params(S, K)
+    march = native.march_params(S, K, skip_escaped=args.skip_escaped == "on")
     ctx = rmr.context()
     total_steps = args.warmup + args.steps
     progress = {"i": 0}
@@ -136,6 +143,8 @@ def main():
     torch.cuda.synchronize()
     ctx.collect_timing(reset=True)
     ctx.timing(True)
+    ctx.stats(True)
+    ctx.collect_stats(reset=True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -148,6 +157,9 @@ def main():
     elapsed = time.perf_counter() - t0
     ctx.timing(False)
     kern_ms, launches = ctx.collect_timing(reset=True)
+    blocks_run, blocks_skipped = ctx.collect_stats(reset=True)
+    ctx.stats(False)
+    skipped_frac = blocks_skipped / max(blocks_run, 1)
     if dist is not None:
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -163,8 +175,9 @@ def main():
     finite = bool(torch.isfinite(model.raw).all().item()) and bool(torch.isfinite(loss).all().item())
 
     # ---- roofline of the dominant kernel -------------------------------------------------
+    # algorithmic work actually executed: escaped blocks run no sphere evaluation at all
     flop_per_ray = FLOP_PER_EVAL * (S + 10) * M
-    flops_launch = flop_per_ray * rays_per_rank
+    flops_launch = flop_per_ray * rays_per_rank * (1.0 - skipped_frac)
     achieved_tf = flops_launch / (kern_avg_ms * 1e-3) / 1e12
     mpad = (M + 31) // 32 * 32
     blocks = (rays_per_rank + 255) // 256
@@ -194,6 +207,7 @@ def main():
         "launches_timed": launches,
         "flop_per_ray": flop_per_ray,
         "rays_per_launch": rays_per_rank,
+        "executed_frac": round(1.0 - skipped_frac, 4),
         "hbm": {"algorithmic_bytes_per_launch": alg_bytes,
                 "achieved_GBs": round(alg_bytes / (kern_avg_ms * 1e-3) / 1e9, 2),
                 "peak_GBs": PEAK_HBM_GBS,
@@ -225,6 +239,8 @@ def main():
                        "views_per_gpu": vpg, "rays_per_step": rays_global, "parallelism": f"views-dp{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "escape_skip": {"enabled": args.skip_escaped == "on", "blocks": blocks_run,
+                            "blocks_skipped": blocks_skipped, "skipped_frac": round(skipped_frac, 4)},
             "finite": finite,
         }
         print(json.dumps(line))

@@ -55,6 +55,12 @@ struct KArgs {
   long long ray_begin;  // first ray of this launch
   long long n_rays;     // rays in this launch
   int width, height, num_views;
+  int tiling;  // camera mode pixel order: 2 = 16x16 tile per block (8x8 per wave), 0 = rows
+  int cull;    // skip blocks whose rays provably escape the scene (RM_MARCH_SKIP_ESCAPED)
+  float cull_min_d;  // scene distance at which the silhouette mask is exactly 0
+  float cull_slack;  // ln(M) / k (rounded up): soft-min minus hard-min bound
+  unsigned long long* stats;  // nullable: [0] += 1 per escaped (skipped) block
+  const int* esc_flags;       // nullable: per-block escape flags of this launch (rm_escape_kernel)
   CamBasis cams[RM_MAX_VIEWS_PER_CALL];
   // activated scene
   const float* centers;
@@ -280,6 +286,175 @@ __device__ __forceinline__ void shade_sweep(const float p[3], const Lds& L, int 
 }
 
 // ---- the fused per-ray kernel ----------------------------------------------------------
+// Bounding sphere of the scene, block-wide: c0 = centre of the centres' bounding box,
+// R >= |c_j - c0| + r_j for every sphere (rounded up). scratch: >= 8*kWaves floats of LDS.
+__device__ __forceinline__ void scene_bound(const KArgs& a, float* scratch, int tid, float c0[3], float& R) {
+  const int lane = tid & 63, wave = tid >> 6;
+  float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (int j = tid; j < a.M; j += kBlock)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float c = a.centers[3 * j + k];
+      v[k] = fminf(v[k], c);
+      v[3 + k] = fmaxf(v[3 + k], c);
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      v[k] = fminf(v[k], __shfl_xor(v[k], off));
+      v[3 + k] = fmaxf(v[3 + k], __shfl_xor(v[3 + k], off));
+    }
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) scratch[8 * wave + k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    float lo = scratch[k], hi = scratch[3 + k];
+    for (int w = 1; w < kWaves; ++w) {
+      lo = fminf(lo, scratch[8 * w + k]);
+      hi = fmaxf(hi, scratch[8 * w + 3 + k]);
+    }
+    c0[k] = 0.5f * (lo + hi);
+  }
+  float r = 0.0f;
+  for (int j = tid; j < a.M; j += kBlock) {
+    const float dx = a.centers[3 * j] - c0[0], dy = a.centers[3 * j + 1] - c0[1], dz = a.centers[3 * j + 2] - c0[2];
+    r = fmaxf(r, sqrtf(dx * dx + dy * dy + dz * dz) + a.radius[j]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) r = fmaxf(r, __shfl_xor(r, off));
+  __syncthreads();  // everyone has read the box
+  if (lane == 0) scratch[8 * wave] = r;
+  __syncthreads();
+  R = scratch[0];
+  for (int w = 1; w < kWaves; ++w) R = fmaxf(R, scratch[8 * w]);
+  R = R * (1.0f + 1e-5f) + 1e-6f;  // cover the f32 rounding of |c - c0| + r
+  __syncthreads();  // scratch is reused by the caller
+}
+
+// Does the ray provably end (after `steps` march steps, or at the given march t) at scene
+// distance >= min_d, beyond its closest approach to the scene's bounding sphere (c0, R)?
+//  * Every sphere distance is >= |p - c0| - R, and the soft-min is >= the hard min minus
+//    ln(M)/k (sdf.rs:30-44), so g(t) = |o + d t - c0| - R - ln(M)/k never exceeds the march
+//    step D(t). Shrinking g by a relative 1e-5 and an absolute 1e-5 (R + |c0| + 1) covers the
+//    f32 rounding of the march (expansion-form distances err by ~6e-8 |p|).
+//  * t + g(t) is non-decreasing (g is (1 - 1e-5)-Lipschitz), so the f64 march of g alone,
+//    tau <- tau + g(tau), stays below the real t at every step (induction from t = tau = 0).
+//  * Past the closest approach g only grows; so tau_S >= t_closest and g(tau_S) >= min_d give
+//    D >= min_d at the march end, at the reconnected point t + D (renderer_diff.rs:30-39) and
+//    hence for the mask, which is then exactly 0 -- as are out and every gradient term.
+__device__ __forceinline__ bool escapes(const float o[3], const float d[3], float t_given, bool have_t, int steps,
+                                     const float c0[3], float R, float slack, float min_d) {
+  const double eps = 1e-5;
+  const double ox = (double)o[0] - c0[0], oy = (double)o[1] - c0[1], oz = (double)o[2] - c0[2];
+  const double dx = d[0], dy = d[1], dz = d[2];
+  const double Rs = (double)R + (double)slack;
+  const double K = eps * (Rs + sqrt((double)c0[0] * c0[0] + (double)c0[1] * c0[1] + (double)c0[2] * c0[2]) + 1.0);
+  auto g = [&](double tt) {
+    const double x = fma(dx, tt, ox), y = fma(dy, tt, oy), z = fma(dz, tt, oz);
+    return (1.0 - eps) * (sqrt(x * x + y * y + z * z) - Rs) - K;
+  };
+  const double tc = -(ox * dx + oy * dy + oz * dz) / (dx * dx + dy * dy + dz * dz);
+  double tau = 0.0;
+  if (have_t) {
+    tau = t_given;
+  } else {
+    for (int s = 0; s < steps; ++s) tau += g(tau);
+  }
+  return tau >= tc && g(tau) >= (double)min_d;
+}
+
+// A block of escaping rays: out = 0 (requested outputs), zero gradient partials, and for the
+// train step the L1 loss of out = 0, reduced exactly as in the full path.
+template <int MODE>
+__device__ __forceinline__ void escaped_block(const KArgs& a, const Lds& L, long long ri, bool valid, int tid, int lane,
+                                           int wave) {
+  if (MODE != kBwd && a.out != nullptr && valid) {
+    a.out[3 * ri] = 0.0f;
+    a.out[3 * ri + 1] = 0.0f;
+    a.out[3 * ri + 2] = 0.0f;
+  }
+  if constexpr (MODE == kFwd || MODE == kRender) return;
+  float* rec = a.partials + (long long)blockIdx.x * a.rec;
+  for (long long e = tid; e < (long long)a.Mpad * 12; e += kBlock) rec[e] = 0.0f;
+  float loss = 0.0f;
+  if (MODE == kTrain && valid) {  // training.rs:17-34 with out = 0
+    const float t0 = a.targets[3 * ri], t1 = a.targets[3 * ri + 1], t2 = a.targets[3 * ri + 2];
+    const float W = (t0 + t1 + t2) > 0.01f ? 10.0f : fmaf(a.progress, 4.0f, 1.0f);
+    const float tg[3] = {t0, t1, t2};
+#pragma unroll
+    for (int c = 0; c < 3; ++c) loss = fmaf(fabsf(0.0f - tg[c]), W, loss);
+  }
+  const float vals[8] = {0.0f, 0.0f, 0.0f, 0.0f, loss, 0.0f, 0.0f, 0.0f};
+  const float red = wave_reduce8(vals, lane);
+  if ((lane & 7) == 7) L.slots[wave * 8 + (lane >> 3)] = red;
+  __syncthreads();
+  if (tid < 8) {
+    float acc = L.slots[tid];
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w) acc += L.slots[w * 8 + tid];
+    rec[(long long)a.Mpad * 12 + tid] = acc;
+  }
+}
+
+// Ray of thread row ri (camera.rs:58-87 in camera mode). In camera mode ri is remapped from
+// the launch order (16x16 pixel tiles per block, 8x8 per wave) to the pixel's row of the
+// [N,3] tensors.
+template <bool CAM>
+__device__ __forceinline__ void setup_ray(const KArgs& a, long long& ri, float o[3], float d[3]) {
+  if constexpr (CAM) {
+    const long long npix = (long long)a.width * a.height;
+    const int v = (int)(ri / npix);
+    const long long pix = ri - (long long)v * npix;
+    int x, y;
+    if (a.tiling == 2) {
+      // a block takes a 16x16 tile, each wave an 8x8 quadrant: compact ray bundles keep the
+      // wave-uniform fast paths on and let whole blocks pass the escape test
+      const long long tl = pix >> 8;
+      const int w = (int)(pix & 255), tiles_x = a.width >> 4;
+      const int ty = (int)(tl / tiles_x), tx = (int)(tl - (long long)ty * tiles_x);
+      const int qd = w >> 6, l = w & 63;
+      y = (ty << 4) + ((qd >> 1) << 3) + (l >> 3);
+      x = (tx << 4) + ((qd & 1) << 3) + (l & 7);
+    } else {
+      y = (int)(pix / a.width);
+      x = (int)(pix - (long long)y * a.width);
+    }
+    ri = (long long)v * npix + (long long)y * a.width + x;
+    camera_ray(a.cams[v], x, y, a.width, a.height, o, d);
+  } else {
+    o[0] = a.org[3 * ri];
+    o[1] = a.org[3 * ri + 1];
+    o[2] = a.org[3 * ri + 2];
+    d[0] = a.dir[3 * ri];
+    d[1] = a.dir[3 * ri + 1];
+    d[2] = a.dir[3 * ri + 2];
+  }
+}
+
+// Escape pre-pass (RM_MARCH_SKIP_ESCAPED): one thread per ray of the coming per-ray launch
+// (same blocks, same rays); flags[b] = 1 when every ray of block b escapes. Kept out of the
+// per-ray kernel so its f64 arithmetic costs that kernel no registers.
+template <int MODE, bool CAM>
+__global__ __launch_bounds__(kBlock) void rm_escape_kernel(const KArgs a, int* __restrict__ flags) {
+  __shared__ float scratch[8 * kWaves];
+  const int tid = threadIdx.x;
+  const long long li = (long long)blockIdx.x * kBlock + tid;
+  const bool valid = li < a.n_rays;
+  long long ri = a.ray_begin + (valid ? li : 0);
+  float o[3], d[3];
+  setup_ray<CAM>(a, ri, o, d);
+  float c0[3], R;
+  scene_bound(a, scratch, tid, c0, R);
+  const bool have_t = MODE == kBwd && a.t_in != nullptr;
+  const bool esc = !valid || escapes(o, d, have_t ? a.t_in[ri] : -1.0f, have_t, a.steps, c0, R, a.cull_slack,
+                                     a.cull_min_d);
+  const int all = __syncthreads_and(esc);
+  if (tid == 0) flags[blockIdx.x] = all;
+}
+
 template <int MODE, bool CAM>
 __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -296,26 +471,22 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long long li = (long long)blockIdx.x * kBlock + tid;
   const bool valid = li < a.n_rays;
-  const long long ri = a.ray_begin + (valid ? li : 0);
+  long long ri = a.ray_begin + (valid ? li : 0);  // becomes the ray's row in the [N,3] tensors
 
   const float kappa = a.k * kLog2e, nkappa = -kappa, inv_kappa = 1.0f / kappa;
   const bool multi = a.Mpad > tile;
 
   // ray (camera.rs:58-87 in camera mode)
   float o[3], d[3];
-  if constexpr (CAM) {
-    const long long npix = (long long)a.width * a.height;
-    const int v = (int)(ri / npix);
-    const long long pix = ri - (long long)v * npix;
-    const int y = (int)(pix / a.width), x = (int)(pix - (long long)y * a.width);
-    camera_ray(a.cams[v], x, y, a.width, a.height, o, d);
-  } else {
-    o[0] = a.org[3 * ri];
-    o[1] = a.org[3 * ri + 1];
-    o[2] = a.org[3 * ri + 2];
-    d[0] = a.dir[3 * ri];
-    d[1] = a.dir[3 * ri + 1];
-    d[2] = a.dir[3 * ri + 2];
+  setup_ray<CAM>(a, ri, o, d);
+
+  // ---- escape skip (RM_MARCH_SKIP_ESCAPED): a block whose rays all provably leave the scene
+  // (rm_escape_kernel) gets out = 0 and zero gradients without marching -- exactly what the full
+  // computation yields for them, since their silhouette mask is 0 in f32 (see escapes()).
+  if (a.esc_flags != nullptr && a.esc_flags[blockIdx.x]) {
+    if (a.stats != nullptr && tid == 0) atomicAdd(a.stats, 1ull);
+    escaped_block<MODE>(a, L, ri, valid, tid, lane, wave);
+    return;
   }
 
   // Minimum sphere radius of the scene (single-tile case): with it, a lower bound on the scene
@@ -961,6 +1132,9 @@ struct rm_context {
   bool timing = false;  // record hipEvents around every per-ray kernel launch
   std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
   size_t events_used = 0;
+  unsigned long long* stats_dev = nullptr;  // escaped-block counter (rm_stats_enable)
+  int* esc_flags = nullptr;                 // per-block escape flags, kMaxBlocksPerLaunch ints
+  long long stats_blocks = 0;               // ray blocks launched while stats are on
 };
 
 namespace {
@@ -1089,6 +1263,14 @@ struct Call {
 };
 
 template <int MODE>
+void launch_escape(bool cam, dim3 grid, hipStream_t st, const KArgs& a, int* flags) {
+  if (cam)
+    hipLaunchKernelGGL((rm_escape_kernel<MODE, true>), grid, dim3(kBlock), 0, st, a, flags);
+  else
+    hipLaunchKernelGGL((rm_escape_kernel<MODE, false>), grid, dim3(kBlock), 0, st, a, flags);
+}
+
+template <int MODE>
 void launch_ray(bool cam, dim3 grid, size_t lds, hipStream_t st, const KArgs& a) {
   if (cam)
     hipLaunchKernelGGL((rm_ray_kernel<MODE, true>), grid, dim3(kBlock), lds, st, a);
@@ -1113,6 +1295,9 @@ int run(rm_context* ctx, const Call& c) {
       if ((rc = make_basis(ctx, c.cams[v], c.W, c.H, a.cams[v])) != RM_OK) return rc;
     a.width = c.W;
     a.height = c.H;
+    // Row order measures fastest for full work (314 vs 304 Mrays/s with 16x16 tiles at the
+    // metric config); compact 16x16 tiles only pay when whole blocks can be skipped.
+    a.tiling = (c.W % 16 == 0 && c.H % 16 == 0) ? 2 : 0;
     a.num_views = c.views;
   } else {
     if (c.n < 0) return fail(ctx, RM_ERR_INVALID_ARG, "num_rays %lld < 0", c.n);
@@ -1151,6 +1336,13 @@ int run(rm_context* ctx, const Call& c) {
   a.progress = c.progress;
   a.inv_count = c.inv_count;
   a.dbg = c.dbg;
+  // Escape skipping needs the mask to be exactly 0 at the certified distance: sigmoid(-msharp D)
+  // once msharp log2(e) D > 128 overflows exp2 (use 160), exp(-10 D^2) in kRender long before 50.
+  const bool mask_vanishes = c.mode == kRender || a.msharp > 0.0f;
+  a.cull = ((c.march->flags & RM_MARCH_SKIP_ESCAPED) != 0 && mask_vanishes && !c.t_out && !c.dbg) ? 1 : 0;
+  a.cull_min_d = c.mode == kRender ? 50.0f : std::max(50.0f, 160.0f / (a.msharp * 1.44269504f));
+  a.cull_slack = (float)(std::log((double)M) / (double)a.k * (1.0 + 1e-6)) + 1e-7f;
+  if (!a.cull && (c.march->flags & RM_MARCH_TILE16) == 0) a.tiling = 0;
   if (c.mode == kRender) {  // renderer.rs:27-32, normalised in f32 on the host like the reference
     const float lv[3] = {-0.5f, 0.5f, -1.0f};
     const float len = std::sqrt(lv[0] * lv[0] + lv[1] * lv[1] + lv[2] * lv[2]);
@@ -1176,6 +1368,19 @@ int run(rm_context* ctx, const Call& c) {
     a.ray_begin = done;
     a.n_rays = nr;
     a.partials = P;
+    a.stats = ctx->stats_dev;
+    if (ctx->stats_dev) ctx->stats_blocks += nb;
+    a.esc_flags = nullptr;
+    if (nb > 0 && a.cull) {
+      if (!ctx->esc_flags) RM_HIP(ctx, hipMalloc(&ctx->esc_flags, sizeof(int) * kMaxBlocksPerLaunch));
+      const dim3 g((unsigned)nb);
+      if (c.mode == kFwd) launch_escape<kFwd>(c.cam, g, ctx->stream, a, ctx->esc_flags);
+      else if (c.mode == kBwd) launch_escape<kBwd>(c.cam, g, ctx->stream, a, ctx->esc_flags);
+      else if (c.mode == kTrain) launch_escape<kTrain>(c.cam, g, ctx->stream, a, ctx->esc_flags);
+      else launch_escape<kRender>(c.cam, g, ctx->stream, a, ctx->esc_flags);
+      RM_HIP(ctx, hipGetLastError());
+      a.esc_flags = ctx->esc_flags;
+    }
     if (nb > 0) {
       hipEvent_t ev0 = nullptr, ev1 = nullptr;
       if (ctx->timing) {
@@ -1279,8 +1484,42 @@ int rm_timing_collect(rm_context* ctx, double* total_ms, int64_t* launches, int3
   return RM_OK;
 }
 
+int rm_stats_enable(rm_context* ctx, int32_t enable) {
+  if (!ctx) return RM_ERR_INVALID_ARG;
+  if (enable && !ctx->stats_dev) {
+    RM_HIP(ctx, hipMalloc(&ctx->stats_dev, sizeof(unsigned long long)));
+    RM_HIP(ctx, hipMemsetAsync(ctx->stats_dev, 0, sizeof(unsigned long long), ctx->stream));
+    ctx->stats_blocks = 0;
+  } else if (!enable && ctx->stats_dev) {
+    RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    RM_HIP(ctx, hipFree(ctx->stats_dev));
+    ctx->stats_dev = nullptr;
+  }
+  return RM_OK;
+}
+
+int rm_stats_collect(rm_context* ctx, int64_t* blocks, int64_t* blocks_skipped, int32_t reset) {
+  if (!ctx || !blocks || !blocks_skipped) return RM_ERR_INVALID_ARG;
+  if (!ctx->stats_dev) return fail(ctx, RM_ERR_INVALID_ARG, "stats are not enabled");
+  unsigned long long v = 0;
+  RM_HIP(ctx, hipMemcpyAsync(&v, ctx->stats_dev, sizeof v, hipMemcpyDeviceToHost, ctx->stream));
+  RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  *blocks = ctx->stats_blocks;
+  *blocks_skipped = (int64_t)v;
+  if (reset) {
+    RM_HIP(ctx, hipMemsetAsync(ctx->stats_dev, 0, sizeof v, ctx->stream));
+    ctx->stats_blocks = 0;
+  }
+  return RM_OK;
+}
+
 void rm_destroy(rm_context* ctx) {
   if (!ctx) return;
+  if (ctx->stats_dev || ctx->esc_flags) {
+    (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->stats_dev) (void)hipFree(ctx->stats_dev);
+    if (ctx->esc_flags) (void)hipFree(ctx->esc_flags);
+  }
   for (auto& pr : ctx->events) {
     (void)hipEventDestroy(pr.first);
     (void)hipEventDestroy(pr.second);
@@ -1301,6 +1540,7 @@ void rm_march_default(rm_march* m) {
   m->normal_eps = 1e-4f;     // scene.rs:91
   m->color_sharpness = 10.0f; // renderer_diff.rs:74
   m->mask_sharpness = 15.0f;  // renderer_diff.rs:88
+  m->flags = 0;
 }
 
 int rm_reserve(rm_context* ctx, int64_t max_rays, int32_t max_spheres) {

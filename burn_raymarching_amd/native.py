@@ -30,7 +30,11 @@ class RmScene(ctypes.Structure):
 
 class RmMarch(ctypes.Structure):
     _fields_ = [("steps", _I32), ("smooth_k", _F), ("normal_eps", _F), ("color_sharpness", _F),
-                ("mask_sharpness", _F)]
+                ("mask_sharpness", _F), ("flags", _I32)]
+
+
+RM_MARCH_SKIP_ESCAPED = 1
+RM_MARCH_TILE16 = 2
 
 
 class RmCamera(ctypes.Structure):
@@ -70,6 +74,8 @@ SIGNATURES = {
                                               ctypes.POINTER(RmMarch), _P]),
     "rm_timing_enable": (ctypes.c_int, [_P, _I32]),
     "rm_timing_collect": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64), _I32]),
+    "rm_stats_enable": (ctypes.c_int, [_P, _I32]),
+    "rm_stats_collect": (ctypes.c_int, [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), _I32]),
     "rm_scene_activate": (ctypes.c_int, [_P, _P, _I32, _P]),
     "rm_scene_from_packed": (None, [_P, _I32, ctypes.POINTER(RmScene)]),
     "rm_grads_from_packed": (None, [_P, _I32, ctypes.POINTER(RmGrads)]),
@@ -142,6 +148,16 @@ class Context:
                    "rm_timing_collect")
         return ms.value, n.value
 
+    def stats(self, enable: bool = True):
+        self.check(self._lib.rm_stats_enable(self.handle, 1 if enable else 0), "rm_stats_enable")
+
+    def collect_stats(self, reset: bool = True):
+        """(ray blocks launched, blocks skipped as escaping) since the last reset."""
+        b, s = _I64(), _I64()
+        self.check(self._lib.rm_stats_collect(self.handle, ctypes.byref(b), ctypes.byref(s), 1 if reset else 0),
+                   "rm_stats_collect")
+        return b.value, s.value
+
     def close(self):
         if getattr(self, "handle", None) is not None and self.handle.value:
             self._lib.rm_destroy(self.handle)
@@ -154,8 +170,16 @@ class Context:
             pass
 
 
-def march_params(steps=40, smooth_k=32.0, normal_eps=1e-4, color_sharpness=10.0, mask_sharpness=15.0) -> RmMarch:
-    return RmMarch(int(steps), float(smooth_k), float(normal_eps), float(color_sharpness), float(mask_sharpness))
+def march_params(steps=40, smooth_k=32.0, normal_eps=1e-4, color_sharpness=10.0, mask_sharpness=15.0,
+                 skip_escaped=None) -> RmMarch:
+    """rm_march; skip_escaped None = the process default (env RM_SKIP_ESCAPED=1, else off);
+    env RM_TILE16=1 adds RM_MARCH_TILE16 (camera-mode pixel order of the skip, for A/B tests)."""
+    if skip_escaped is None:
+        skip_escaped = os.environ.get("RM_SKIP_ESCAPED", "0") == "1"
+    flags = (RM_MARCH_SKIP_ESCAPED if skip_escaped else 0) | (RM_MARCH_TILE16 if os.environ.get("RM_TILE16") == "1"
+                                                              else 0)
+    return RmMarch(int(steps), float(smooth_k), float(normal_eps), float(color_sharpness), float(mask_sharpness),
+                   flags)
 
 
 def cameras(cams) -> ctypes.Array:

@@ -66,7 +66,22 @@ typedef struct rm_march {
   float normal_eps;       /* finite-difference normal step, scene.rs:91 (1e-4)       */
   float color_sharpness;  /* softmax(-c * dist) colour blend, renderer_diff.rs:74 (10) */
   float mask_sharpness;   /* sigmoid(-c * D) silhouette, renderer_diff.rs:88 (15)     */
+  int32_t flags;          /* RM_MARCH_* bits (default 0)                              */
 } rm_march;
+
+/* Skip the per-sphere work of ray blocks that provably escape the scene: every ray of the
+ * block ends its march past the scene's bounding sphere at a distance where the silhouette
+ * mask is exactly 0 in f32, so out = 0 and all its gradient terms are 0 -- the values the full
+ * computation produces. The proof is a conservative f64 march of a bounding-sphere lower bound
+ * in a pre-pass kernel (escapes() in rm_kernels.hip); camera mode then renders 16x16 pixel
+ * tiles per block. Pays for compact scenes seen in camera mode (previews, target generation);
+ * off by default because the pre-pass and the uneven block costs lose when few blocks escape.
+ * Ignored when t_march or debug outputs are requested. */
+#define RM_MARCH_SKIP_ESCAPED 1
+/* Camera mode: launch 16x16 pixel tiles per 256-ray block (8x8 per wave) instead of rows
+ * (implied by RM_MARCH_SKIP_ESCAPED; needs width and height multiples of 16). Changes only the
+ * summation order of the gradients. */
+#define RM_MARCH_TILE16 2
 
 /* Pinhole LookAt camera, camera.rs:30-37. Rays are generated in-kernel exactly as
  * create_camera_rays (camera.rs:41-87): rows y then x, u = x/W*2-1, v = -(y/H*2-1). */
@@ -171,6 +186,13 @@ int rm_debug_intermediates(rm_context* ctx, const float* ray_org, const float* r
  * time in milliseconds and the number of launches (reset != 0 clears the record). */
 int rm_timing_enable(rm_context* ctx, int32_t enable);
 int rm_timing_collect(rm_context* ctx, double* total_ms, int64_t* launches, int32_t reset);
+
+/* ---- work statistics -------------------------------------------------------- */
+/* rm_stats_enable(ctx, 1): count, for every later per-ray launch, the ray blocks (256 rays)
+ * launched and those skipped by RM_MARCH_SKIP_ESCAPED. rm_stats_collect synchronises the
+ * stream; reset != 0 clears both counters. */
+int rm_stats_enable(rm_context* ctx, int32_t enable);
+int rm_stats_collect(rm_context* ctx, int64_t* blocks, int64_t* blocks_skipped, int32_t reset);
 
 /* ---- model helpers: SceneModel activations, compute_loss penalties, Adam ---- */
 /* Packed parameter layout used by the helpers (raw Param tensors or their grads):

@@ -49,6 +49,7 @@ def test_version_and_defaults(native):
     lib.rm_march_default(ctypes.byref(m))
     assert m.steps == 40 and m.smooth_k == 32.0  # renderer_diff.rs:22, train.rs:131
     assert m.normal_eps == np.float32(1e-4) and m.color_sharpness == 10.0 and m.mask_sharpness == 15.0
+    assert m.flags == 0  # RM_MARCH_SKIP_ESCAPED is opt-in
 
 
 def test_null_context_is_rejected(native):

@@ -53,4 +53,8 @@ def test_gpu_matches_golden(path):
     for key, tol in GRAD_TOL.items():
         ref = z[f"grad_{key}_f64"].reshape(-1)
         err = np.abs(gr[key].cpu().numpy().reshape(-1) - ref).max()
-        assert err <= tol * np.abs(ref).max(), (key, err)
+        # the bar is the stated tolerance, or twice the error of the reference's own f32 op order
+        # where that is larger (light_dir with a random upstream gradient sums n over rays with
+        # cancelling signs: the f32 restatement is 8e-2 off at S=16, k=5)
+        f32_err = np.abs(z[f"grad_{key}_f32"].astype(np.float64).reshape(-1) - ref).max()
+        assert err <= max(tol * np.abs(ref).max(), 2.0 * f32_err), (key, err, f32_err)
