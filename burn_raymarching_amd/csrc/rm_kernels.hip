@@ -58,7 +58,7 @@ struct KArgs {
   int tiling;  // camera mode pixel order: 2 = 16x16 tile per block (8x8 per wave), 0 = rows
   int cull;    // skip blocks whose rays provably escape the scene (RM_MARCH_SKIP_ESCAPED)
   float cull_min_d;  // scene distance at which the silhouette mask is exactly 0
-  float cull_slack;  // ln(M) / k (rounded up): soft-min minus hard-min bound
+  float lse_slack;  // ln(M) / k (rounded up): the hard min exceeds the soft-min by at most this
   unsigned long long* stats;  // nullable: [0] += 1 per escaped (skipped) block
   const int* esc_flags;       // nullable: per-block escape flags of this launch (rm_escape_kernel)
   CamBasis cams[RM_MAX_VIEWS_PER_CALL];
@@ -104,9 +104,14 @@ __host__ __device__ constexpr size_t lds_bytes(int tile) {
   return (size_t)tile * 36 + (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float) + 64;
 }
 
-// Stages spheres [t0, t0 + tn) (tn even); returns this thread's minimum real radius.
-__device__ __forceinline__ float stage_tile(const KArgs& a, const Lds& L, int t0, int tn, float kappa) {
+// Stages spheres [t0, t0 + tn) (tn even); returns this thread's minimum real radius and, via
+// rmax / cspread, its maximum radius and maximum |c_j - c_0| (c_0 = sphere 0's centre).
+__device__ __forceinline__ float stage_tile(const KArgs& a, const Lds& L, int t0, int tn, float kappa, float& rmax,
+                                            float& cspread) {
   float rmin = INFINITY;
+  rmax = 0.0f;
+  cspread = 0.0f;
+  const float c0x = a.centers[0], c0y = a.centers[1], c0z = a.centers[2];
   for (int ip = threadIdx.x; ip < tn / 2; ip += kBlock) {
     float gx[2], gy[2], gz[2], cc[2], kr[2], rr[2], cr[2], cg[2], cb[2];
 #pragma unroll
@@ -125,6 +130,9 @@ __device__ __forceinline__ float stage_tile(const KArgs& a, const Lds& L, int t0
         cg[h] = a.colors[3 * j + 1];
         cb[h] = a.colors[3 * j + 2];
         rmin = fminf(rmin, r);
+        rmax = fmaxf(rmax, r);
+        const float ex = cx - c0x, ey = cy - c0y, ez = cz - c0z;
+        cspread = fmaxf(cspread, sqrtf(ex * ex + ey * ey + ez * ez));
       } else {
         // padding sphere at c = (kPadCenter, 0, 0): the expansion form (|c|^2) and the direct
         // form of the normal taps (p - c) both see distance ~1e15, so every exp() of its terms
@@ -166,7 +174,14 @@ __device__ __forceinline__ float psq(const float p[3]) { return fmaf(p[2], p[2],
 // Base-2 log-sum-exp of v_j = kappa*(r_j - rho_j) over a tile (sdf.rs:36-40), running max m and
 // shifted sum s carried across tiles; chunks of 16 spheres, one rescale exp per chunk.
 // CLAMP=false drops max(q, 1e-6): only used when the caller proved every rho_j >= kSafeRho.
-template <bool CLAMP>
+// Shift of the exponents: kShiftMax = chunked running max (always safe); kShiftFixed = m set
+// once from the first sphere (safe when kappa * (r_max + max |c_j - c_0|) <= 100 and the point
+// is near enough that fp32 rounding of rho stays small, so every exponent lies within +-100 of
+// it); kShiftNone = m = 0 (safe when the hard maximum is known to lie in [-100, 100]). All three
+// give the same log-sum-exp up to fp32 rounding.
+enum LseShift { kShiftMax = 0, kShiftFixed = 1, kShiftNone = 2 };
+
+template <bool CLAMP, int SHIFT>
 __device__ __forceinline__ void lse_point(const float p[3], const Lds& L, int npairs, float nkappa, float& m,
                                           float& s) {
   const f2 PX = sp(p[0]), PY = sp(p[1]), PZ = sp(p[2]), PP = sp(psq(p)), NK = sp(nkappa);
@@ -179,6 +194,17 @@ __device__ __forceinline__ void lse_point(const float p[3], const Lds& L, int np
       f2 q = qpair(PX, PY, PZ, PP, A, B);
       if constexpr (CLAMP) q = clamp_q(q);
       v[ii] = fma2(sqrt2(q), NK, f2{K.x, K.y});
+    }
+    if constexpr (SHIFT != kShiftMax) {
+      if constexpr (SHIFT == kShiftFixed) {
+        if (m == -INFINITY) m = v[0].x;
+      }
+      const f2 MN = sp(m);
+      f2 acc = f2{s, 0.0f};
+#pragma unroll
+      for (int ii = 0; ii < 8; ++ii) acc += exp2v(SHIFT == kShiftNone ? v[ii] : v[ii] - MN);
+      s = acc.x + acc.y;
+      continue;
     }
     float cm = fmaxf(v[0].x, v[0].y);
 #pragma unroll
@@ -449,7 +475,7 @@ __global__ __launch_bounds__(kBlock) void rm_escape_kernel(const KArgs a, int* _
   float c0[3], R;
   scene_bound(a, scratch, tid, c0, R);
   const bool have_t = MODE == kBwd && a.t_in != nullptr;
-  const bool esc = !valid || escapes(o, d, have_t ? a.t_in[ri] : -1.0f, have_t, a.steps, c0, R, a.cull_slack,
+  const bool esc = !valid || escapes(o, d, have_t ? a.t_in[ri] : -1.0f, have_t, a.steps, c0, R, a.lse_slack,
                                      a.cull_min_d);
   const int all = __syncthreads_and(esc);
   if (tid == 0) flags[blockIdx.x] = all;
@@ -493,15 +519,34 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   // distance proves rho_j = dist_j + r_j >= kSafeRho for every sphere, so max(q, 1e-6) cannot
   // bind and the sweeps may skip it (exactly the same results). Multi-tile: fast path off.
   float rmin = -INFINITY;
+  // Block-uniform permissions for the cheaper log-sum-exp shifts of the march (lse_point).
+  bool shift_fixed_ok = false, shift_none_ok = false;
   if (!multi) {
-    float rl = stage_tile(a, L, 0, a.Mpad, kappa);
+    float rmx, spr;
+    float rl = stage_tile(a, L, 0, a.Mpad, kappa, rmx, spr);
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) rl = fminf(rl, __shfl_xor(rl, off));
-    if (lane == 0) L.misc[wave] = rl;
+    for (int off = 32; off > 0; off >>= 1) {
+      rl = fminf(rl, __shfl_xor(rl, off));
+      rmx = fmaxf(rmx, __shfl_xor(rmx, off));
+      spr = fmaxf(spr, __shfl_xor(spr, off));
+    }
+    if (lane == 0) {
+      L.misc[wave] = rl;
+      L.misc[kWaves + wave] = rmx;
+      L.misc[2 * kWaves + wave] = spr;
+    }
     __syncthreads();
     rmin = L.misc[0];
+    float rmax = L.misc[kWaves], spread = L.misc[2 * kWaves];
 #pragma unroll
-    for (int w = 1; w < kWaves; ++w) rmin = fminf(rmin, L.misc[w]);
+    for (int w = 1; w < kWaves; ++w) {
+      rmin = fminf(rmin, L.misc[w]);
+      rmax = fmaxf(rmax, L.misc[kWaves + w]);
+      spread = fmaxf(spread, L.misc[2 * kWaves + w]);
+    }
+    // |v_j - v_0| = kappa |r_j - r_0 - (rho_j - rho_0)| <= kappa (r_max + |c_j - c_0|); v <= kappa r_max
+    shift_fixed_ok = kappa * (rmax + spread) * 1.001f <= 100.0f;
+    shift_none_ok = kappa * rmax * 1.001f <= 100.0f;
   }
   // Wave-uniform choice of the clamp-free path from a per-lane lower bound on the distance.
   auto all_safe = [&](float dist_lb) { return __all(dist_lb + rmin >= kSafeRho) != 0; };
@@ -512,7 +557,8 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
       const int tn = min(tile, a.Mpad - t0);
       if (multi) {
         __syncthreads();
-        stage_tile(a, L, t0, tn, kappa);
+        float u0, u1;
+        stage_tile(a, L, t0, tn, kappa, u0, u1);
         __syncthreads();
       }
       body(t0, tn);
@@ -523,17 +569,38 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     m = -INFINITY;
     s = 0.0f;
     if (fast)
-      for_tiles([&](int, int tn) { lse_point<false>(p, L, tn / 2, nkappa, m, s); });
+      for_tiles([&](int, int tn) { lse_point<false, kShiftMax>(p, L, tn / 2, nkappa, m, s); });
     else
-      for_tiles([&](int, int tn) { lse_point<true>(p, L, tn / 2, nkappa, m, s); });
+      for_tiles([&](int, int tn) { lse_point<true, kShiftMax>(p, L, tn / 2, nkappa, m, s); });
     return -(flog2(fmaxf(s, 1e-8f)) + m) * inv_kappa;
+  };
+  // The march's soft-min with the cheapest safe shift (the result differs only by fp32 rounding).
+  // kShiftNone needs the hard maximum -kappa d_min >= -100 at the new point: d_min(new) <=
+  // d_min(old) + |D| <= D + ln(M)/k + |D| (the soft-min is within ln(M)/k below the hard min).
+  auto soft_min_march = [&](const float p[3], bool fast, float Dprev) {
+    const bool none = shift_none_ok && __all(2.0f * fmaxf(Dprev, 0.0f) + a.lse_slack <= 90.0f * inv_kappa);
+    float m = none ? 0.0f : -INFINITY, s = 0.0f;
+    if (none) {
+      if (fast) for_tiles([&](int, int tn) { lse_point<false, kShiftNone>(p, L, tn / 2, nkappa, m, s); });
+      else for_tiles([&](int, int tn) { lse_point<true, kShiftNone>(p, L, tn / 2, nkappa, m, s); });
+    } else if (shift_fixed_ok && __all(psq(p) <= 1e10f)) {
+      // |p| <= 1e5: the expansion-form rounding of rho (~1.5 ulp(|p|)) moves the exponents by
+      // < 0.5; far out it can exceed the +-100 headroom, so distant points keep the running max
+      if (fast) for_tiles([&](int, int tn) { lse_point<false, kShiftFixed>(p, L, tn / 2, nkappa, m, s); });
+      else for_tiles([&](int, int tn) { lse_point<true, kShiftFixed>(p, L, tn / 2, nkappa, m, s); });
+    } else {
+      if (fast) for_tiles([&](int, int tn) { lse_point<false, kShiftMax>(p, L, tn / 2, nkappa, m, s); });
+      else for_tiles([&](int, int tn) { lse_point<true, kShiftMax>(p, L, tn / 2, nkappa, m, s); });
+    }
+    return -(flog2(fmaxf(s, 1e-30f)) + m) * inv_kappa;
   };
 
   // ---- march: t <- (t + sdf(o + d t)).detach(), S times (renderer_diff.rs:20-26)
-  // The fast path needs a distance lower bound: the previous point's hard minimum -m/kappa minus
-  // the step just taken (every dist_j is 1-Lipschitz and |d| = 1).
+  // The fast path needs a distance lower bound: the previous point's hard minimum (>= its
+  // soft-min D) minus the step just taken (every dist_j is 1-Lipschitz and |d| = 1).
   float t = 0.0f;
   float lb = -INFINITY;  // lower bound on the scene distance at the current point
+  float Dprev = INFINITY;  // previous march step (none yet)
   if (MODE == kBwd && a.t_in != nullptr) {
     t = a.t_in[ri];
   } else {
@@ -551,10 +618,11 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
       if (st == half) __builtin_amdgcn_s_setprio(2);
 #endif
       const float p[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
-      float m, s;
-      const float D = soft_min(p, all_safe(lb), m, s);
+      const float D = soft_min_march(p, all_safe(lb), Dprev);
       t += D;
-      lb = -m * inv_kappa - fabsf(D);
+      // next point: hard min >= soft-min D here, moved by |D|
+      lb = D - fabsf(D);
+      Dprev = D;
     }
   }
 #if RM_PRIO_RAMP
@@ -1341,7 +1409,7 @@ int run(rm_context* ctx, const Call& c) {
   const bool mask_vanishes = c.mode == kRender || a.msharp > 0.0f;
   a.cull = ((c.march->flags & RM_MARCH_SKIP_ESCAPED) != 0 && mask_vanishes && !c.t_out && !c.dbg) ? 1 : 0;
   a.cull_min_d = c.mode == kRender ? 50.0f : std::max(50.0f, 160.0f / (a.msharp * 1.44269504f));
-  a.cull_slack = (float)(std::log((double)M) / (double)a.k * (1.0 + 1e-6)) + 1e-7f;
+  a.lse_slack = (float)(std::log((double)M) / (double)a.k * (1.0 + 1e-6)) + 1e-7f;
   if (!a.cull && (c.march->flags & RM_MARCH_TILE16) == 0) a.tiling = 0;
   if (c.mode == kRender) {  // renderer.rs:27-32, normalised in f32 on the host like the reference
     const float lv[3] = {-0.5f, 0.5f, -1.0f};
