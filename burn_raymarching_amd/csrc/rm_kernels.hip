@@ -61,6 +61,8 @@ struct KArgs {
   float lse_slack;  // ln(M) / k (rounded up): the hard min exceeds the soft-min by at most this
   unsigned long long* stats;  // nullable: [0] += 1 per escaped (skipped) block
   const int* esc_flags;       // nullable: per-block escape flags of this launch (rm_escape_kernel)
+  int wmarch;                 // the weighted march (records in wrec, see rm_wrec_kernel)
+  const float4* wrec;
   CamBasis cams[RM_MAX_VIEWS_PER_CALL];
   // activated scene
   const float* centers;
@@ -97,7 +99,7 @@ struct Lds {
   float4* P3;
   float2* P4;
   float* slots;  // backward wave partials, 2 buffers
-  float* misc;   // [kWaves] per-wave minimum radius
+  float* misc;   // [3][kWaves] per-wave minimum radius, maximum radius, centre spread
 };
 
 __host__ __device__ constexpr size_t lds_bytes(int tile) {
@@ -150,6 +152,44 @@ __device__ __forceinline__ float stage_tile(const KArgs& a, const Lds& L, int t0
     L.P4[ip] = make_float2(cb[0], cb[1]);
   }
   return rmin;
+}
+
+// Weighted march records for spheres [0, Mpad) (M <= 512), written once per call to global
+// memory and read by the march with wave-uniform addresses, i.e. scalar loads into SGPRs that
+// feed the packed VALU ops directly (no LDS broadcast traffic). Per sphere pair ip:
+//   rec[3 ip + 0] = {-2k^2 cx0, -2k^2 cx1, -2k^2 cy0, -2k^2 cy1}
+//   rec[3 ip + 1] = {-2k^2 cz0, -2k^2 cz1, k^2|c0|^2, k^2|c1|^2}
+//   rec[3 ip + 2] = {2^(k r0), 2^(k r1), 2^(k (r0 - r_first)), 2^(k (r1 - r_first))}
+// so sqrt(q') = k rho and a soft-min term is one packed fma: w * 2^(shift - k rho).
+__global__ __launch_bounds__(256) void rm_wrec_kernel(const KArgs a, float4* __restrict__ rec) {
+  const float kappa = a.k * kLog2e;
+  const float k2 = kappa * kappa;
+  const float kr_first = kappa * a.radius[0];
+  for (int ip = threadIdx.x; ip < a.Mpad / 2; ip += 256) {
+    float gx[2], gy[2], gz[2], cc[2], w[2], wf[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = 2 * ip + h;
+      if (j < a.M) {
+        const float cx = a.centers[3 * j], cy = a.centers[3 * j + 1], cz = a.centers[3 * j + 2];
+        const float kr = kappa * a.radius[j];
+        gx[h] = -2.0f * k2 * cx;
+        gy[h] = -2.0f * k2 * cy;
+        gz[h] = -2.0f * k2 * cz;
+        cc[h] = k2 * (cx * cx + cy * cy + cz * cz);
+        w[h] = fexp2(kr);
+        wf[h] = fexp2(kr - kr_first);
+      } else {  // padding: q' ~ k^2 1e30 and weight 0, its term is exactly 0
+        gx[h] = -2.0f * k2 * kPadCenter;
+        gy[h] = gz[h] = 0.0f;
+        cc[h] = k2 * kPadCenter * kPadCenter;
+        w[h] = wf[h] = 0.0f;
+      }
+    }
+    rec[3 * ip] = make_float4(gx[0], gx[1], gy[0], gy[1]);
+    rec[3 * ip + 1] = make_float4(gz[0], gz[1], cc[0], cc[1]);
+    rec[3 * ip + 2] = make_float4(w[0], w[1], wf[0], wf[1]);
+  }
 }
 
 // ---- packed helpers --------------------------------------------------------------------------
@@ -217,6 +257,40 @@ __device__ __forceinline__ void lse_point(const float p[3], const Lds& L, int np
     s = acc.x + acc.y;
     m = mn;
   }
+}
+
+// The march's log-sum-exp in weighted form: rho' = sqrt(k^2 q) = k rho straight from the scaled
+// geometry, term = 2^(k r_j) 2^(-rho'_j) (FIXED = false: shift 0) or 2^(k (r_j - r_0))
+// 2^(rho'_0 - rho'_j) (FIXED: shift v_0 = k r_0 - rho'_0) -- one packed fma per sphere pair
+// instead of the fma + subtract + add of lse_point. Returns the sum; *sh receives rho'_0.
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(4))) f4v* cf4_ptr;  // constant space: scalar loads
+
+template <bool CLAMP, bool FIXED>
+__device__ __forceinline__ float lse_weighted(const float p[3], const float4* rec_g, int npairs, float k2, float& sh) {
+  const cf4_ptr rec = (cf4_ptr)rec_g;  // read-only in this kernel, wave-uniform addresses
+  const f2 PX = sp(p[0]), PY = sp(p[1]), PZ = sp(p[2]), PP = sp(k2 * psq(p)), QMIN = sp(k2 * 1e-6f);
+  f2 acc[2] = {sp(0.0f), sp(0.0f)}, SH = sp(0.0f);  // two chains keep the fma latency hidden
+  for (int i0 = 0; i0 < npairs; i0 += 8) {
+#pragma unroll
+    for (int ii = 0; ii < 8; ++ii) {
+      const f4v a4 = rec[3 * (i0 + ii)], b4 = rec[3 * (i0 + ii) + 1], w4 = rec[3 * (i0 + ii) + 2];
+      const float4 A = make_float4(a4.x, a4.y, a4.z, a4.w), B = make_float4(b4.x, b4.y, b4.z, b4.w),
+                   Wt = make_float4(w4.x, w4.y, w4.z, w4.w);
+      f2 q = qpair(PX, PY, PZ, PP, A, B);
+      if constexpr (CLAMP) q = f2{fmaxf(q.x, QMIN.x), fmaxf(q.y, QMIN.y)};
+      const f2 rho = sqrt2(q);
+      if constexpr (FIXED) {
+        if (i0 == 0 && ii == 0) SH = sp(rho.x);
+        acc[ii & 1] = fma2(hi(Wt), exp2v(SH - rho), acc[ii & 1]);
+      } else {
+        acc[ii & 1] = fma2(lo(Wt), exp2v(-rho), acc[ii & 1]);
+      }
+    }
+  }
+  sh = SH.x;
+  const f2 t = acc[0] + acc[1];
+  return t.x + t.y;
 }
 
 // The six normal taps p +- eps*e_a (scene.rs:93-111) in one pass over the spheres. q at a tap
@@ -546,8 +620,11 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     }
     // |v_j - v_0| = kappa |r_j - r_0 - (rho_j - rho_0)| <= kappa (r_max + |c_j - c_0|); v <= kappa r_max
     shift_fixed_ok = kappa * (rmax + spread) * 1.001f <= 100.0f;
-    shift_none_ok = kappa * rmax * 1.001f <= 100.0f;
+    // the weighted form 2^(k r) 2^(-k rho) also needs 2^(-k rho) of the nearest sphere normal:
+    // k rho <= 90 + k r_max <= 120
+    shift_none_ok = kappa * rmax * 1.001f <= (a.wmarch ? 30.0f : 100.0f);
   }
+  const float kr_first = kappa * a.radius[0];
   // Wave-uniform choice of the clamp-free path from a per-lane lower bound on the distance.
   auto all_safe = [&](float dist_lb) { return __all(dist_lb + rmin >= kSafeRho) != 0; };
 
@@ -580,10 +657,23 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   auto soft_min_march = [&](const float p[3], bool fast, float Dprev) {
     const bool none = shift_none_ok && __all(2.0f * fmaxf(Dprev, 0.0f) + a.lse_slack <= 90.0f * inv_kappa);
     float m = none ? 0.0f : -INFINITY, s = 0.0f;
+    const bool fixed = !none && shift_fixed_ok && __all(psq(p) <= 1e10f);
+    if (a.wmarch && (none || fixed)) {
+      const float k2 = kappa * kappa;
+      const int np = a.Mpad / 2;
+      float sh;
+      if (none) {
+        s = fast ? lse_weighted<false, false>(p, a.wrec, np, k2, sh) : lse_weighted<true, false>(p, a.wrec, np, k2, sh);
+      } else {
+        s = fast ? lse_weighted<false, true>(p, a.wrec, np, k2, sh) : lse_weighted<true, true>(p, a.wrec, np, k2, sh);
+        m = kr_first - sh;
+      }
+      return -(flog2(fmaxf(s, 1e-30f)) + m) * inv_kappa;
+    }
     if (none) {
       if (fast) for_tiles([&](int, int tn) { lse_point<false, kShiftNone>(p, L, tn / 2, nkappa, m, s); });
       else for_tiles([&](int, int tn) { lse_point<true, kShiftNone>(p, L, tn / 2, nkappa, m, s); });
-    } else if (shift_fixed_ok && __all(psq(p) <= 1e10f)) {
+    } else if (fixed) {
       // |p| <= 1e5: the expansion-form rounding of rho (~1.5 ulp(|p|)) moves the exponents by
       // < 0.5; far out it can exceed the +-100 headroom, so distant points keep the running max
       if (fast) for_tiles([&](int, int tn) { lse_point<false, kShiftFixed>(p, L, tn / 2, nkappa, m, s); });
@@ -1202,6 +1292,7 @@ struct rm_context {
   size_t events_used = 0;
   unsigned long long* stats_dev = nullptr;  // escaped-block counter (rm_stats_enable)
   int* esc_flags = nullptr;                 // per-block escape flags, kMaxBlocksPerLaunch ints
+  float4* wrec = nullptr;                   // weighted march records, 256 pairs
   long long stats_blocks = 0;               // ray blocks launched while stats are on
 };
 
@@ -1417,6 +1508,14 @@ int run(rm_context* ctx, const Call& c) {
     for (int i = 0; i < 3; ++i) a.light_fixed[i] = lv[i] / len;
   }
   a.rec = rec_floats(Mpad);
+  // weighted march records (scalar-loaded, see rm_wrec_kernel) for up to 512 spheres
+  a.wmarch = (Mpad <= tile && Mpad <= 512 && n > 0) ? 1 : 0;
+  if (a.wmarch) {
+    if (!ctx->wrec) RM_HIP(ctx, hipMalloc(&ctx->wrec, sizeof(float4) * 3 * 256));
+    hipLaunchKernelGGL(rm_wrec_kernel, dim3(1), dim3(256), 0, ctx->stream, a, ctx->wrec);
+    RM_HIP(ctx, hipGetLastError());
+    a.wrec = ctx->wrec;
+  }
   const size_t lds = lds_bytes(tile);
 
   if (has_bwd) {
@@ -1583,10 +1682,11 @@ int rm_stats_collect(rm_context* ctx, int64_t* blocks, int64_t* blocks_skipped, 
 
 void rm_destroy(rm_context* ctx) {
   if (!ctx) return;
-  if (ctx->stats_dev || ctx->esc_flags) {
+  if (ctx->stats_dev || ctx->esc_flags || ctx->wrec) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stats_dev) (void)hipFree(ctx->stats_dev);
     if (ctx->esc_flags) (void)hipFree(ctx->esc_flags);
+    if (ctx->wrec) (void)hipFree(ctx->wrec);
   }
   for (auto& pr : ctx->events) {
     (void)hipEventDestroy(pr.first);

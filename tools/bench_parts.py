@@ -37,21 +37,22 @@ def main():
     W = int(os.environ.get("RM_W", "512"))
     M = int(os.environ.get("RM_M", "256"))
     S = int(os.environ.get("RM_S", "32"))
+    V = int(os.environ.get("RM_V", "2"))
     sc = model.scene_tensors(model.synthetic_scene(M, 0))
-    cam = model.ring_cameras(10)[0]
+    cams = model.ring_cameras(10)[:V]
     ctx = render.context()
-    tgt = render.render_diff_camera([cam], W, W, model.scene_tensors(model.synthetic_scene(M, 1)), 32.0, S)
-    _, t = render.render_diff_camera([cam], W, W, sc, 32.0, S, return_t=True)
-    g = torch.randn((W * W, 3), device="cuda")
+    tgt = render.render_diff_camera(cams, W, W, model.scene_tensors(model.synthetic_scene(M, 1)), 32.0, S)
+    _, t = render.render_diff_camera(cams, W, W, sc, 32.0, S, return_t=True)
+    g = torch.randn((V * W * W, 3), device="cuda")
     res = {
-        "fwd_S32": timed(ctx, lambda: render.render_diff_camera([cam], W, W, sc, 32.0, S)),
-        "fwd_S0": timed(ctx, lambda: render.render_diff_camera([cam], W, W, sc, 32.0, 0)),
-        "bwd_t": timed(ctx, lambda: render.render_diff_backward_camera([cam], W, W, sc, 32.0, g, S, t_march=t)),
-        "train": timed(ctx, lambda: render.train_step_camera([cam], W, W, tgt, sc, 32.0, 0.5, S)),
+        "fwd_S32": timed(ctx, lambda: render.render_diff_camera(cams, W, W, sc, 32.0, S)),
+        "fwd_S0": timed(ctx, lambda: render.render_diff_camera(cams, W, W, sc, 32.0, 0)),
+        "bwd_t": timed(ctx, lambda: render.render_diff_backward_camera(cams, W, W, sc, 32.0, g, S, t_march=t)),
+        "train": timed(ctx, lambda: render.train_step_camera(cams, W, W, tgt, sc, 32.0, 0.5, S)),
     }
     res["march_only"] = res["fwd_S32"] - res["fwd_S0"]
     res["backward_sweeps"] = res["bwd_t"] - res["fwd_S0"]
-    res["config"] = {"W": W, "M": M, "S": S}
+    res["config"] = {"W": W, "M": M, "S": S, "V": V}
     print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in res.items()}))
 
 
