@@ -44,7 +44,6 @@ namespace rm {
 // kRender: the non-differentiable target renderer of renderer.rs:4-80 (generate.rs)
 enum Mode { kFwd = 0, kBwd = 1, kTrain = 2, kRender = 3 };
 
-constexpr int kTileMax = 1024;            // spheres per LDS tile (40 B each)
 constexpr int kMaxBlocksPerLaunch = 4096; // bounds the partial-gradient workspace per launch
 constexpr int kReduceSegs = 32;           // block segments of the first reduction pass
 
@@ -61,8 +60,6 @@ struct KArgs {
   float lse_slack;  // ln(M) / k (rounded up): the hard min exceeds the soft-min by at most this
   unsigned long long* stats;  // nullable: [0] += 1 per escaped (skipped) block
   const int* esc_flags;       // nullable: per-block escape flags of this launch (rm_escape_kernel)
-  int wmarch;                 // the weighted march (records in wrec, see rm_wrec_kernel)
-  const float4* wrec;
   CamBasis cams[RM_MAX_VIEWS_PER_CALL];
   // activated scene
   const float* centers;
@@ -70,7 +67,8 @@ struct KArgs {
   const float* radius;
   const float* light_dir;
   const float* ambient;
-  int M, Mpad, tile;
+  int M, Mpad;
+  const float4* rec_buf;  // sphere records of this call (rm_prep_kernel), see Lds
   // march / shading
   int steps;
   float k, eps, csharp, msharp;
@@ -87,38 +85,105 @@ struct KArgs {
   long long rec;
 };
 
-// ---- LDS staging: pair-interleaved sphere records ---------------------------------------
-// Pair i holds spheres (2i, 2i+1) so that every sweep runs two spheres per v_pk_* instruction:
+// ---- sphere records: pair-interleaved, in global memory, read through scalar loads ----------
+// rm_prep_kernel writes them once per call. Pair i holds spheres (2i, 2i+1) so every sweep runs
+// two spheres per v_pk_* instruction:
 //   P0 = {-2cx0, -2cx1, -2cy0, -2cy1}   P1 = {-2cz0, -2cz1, |c0|^2, |c1|^2}
-//   P2 = {kappa r0, kappa r1, r0, r1}    P3 = {red0, red1, green0, green1}   P4 = {blue0, blue1}
-// (36 B per sphere). All lanes of a wave read the same record: LDS broadcast.
-struct Lds {
-  float4* P0;
-  float4* P1;
-  float4* P2;
-  float4* P3;
-  float2* P4;
-  float* slots;  // backward wave partials, 2 buffers
-  float* misc;   // [3][kWaves] per-wave minimum radius, maximum radius, centre spread
-};
+//   P2 = {k r0, k r1, r0, r1}           P3 = {red0, red1, green0, green1}   P4 = {blue0, blue1}
+//   S0, S1 = P0, P1 scaled by k^2       W  = {2^(k r0), 2^(k r1), 2^(k (r0 - r_first)), 2^(k (r1 - r_first))}
+// (k = smooth_k log2 e). Every lane of a wave reads the same record at the same time, so the
+// kernel reads them through the constant address space: s_load into SGPRs that feed the
+// packed VALU ops as scalar operands -- no LDS staging, no LDS broadcast traffic, and no limit
+// on M (the records stream through the scalar cache / L2).
+typedef float f4v __attribute__((ext_vector_type(4)));
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef const __attribute__((address_space(4))) f4v* cf4_ptr;
+typedef const __attribute__((address_space(4))) f2v* cf2_ptr;
+typedef const __attribute__((address_space(4))) float* cf1_ptr;
 
-__host__ __device__ constexpr size_t lds_bytes(int tile) {
-  return (size_t)tile * 36 + (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float) + 64;
+// Header after the records: {r_min, r_max, max |c_j - c_0|, 0} of the real spheres, followed by
+// one partial header per rm_prep_kernel block when that kernel ran on more than one block.
+constexpr int kRecHeader = 4;
+
+__host__ __device__ inline size_t rec_bytes(int npairs, int nprep) {
+  return (size_t)npairs * (7 * 16 + 8) + (size_t)(nprep + 1) * kRecHeader * sizeof(float);
 }
 
-// Stages spheres [t0, t0 + tn) (tn even); returns this thread's minimum real radius and, via
-// rmax / cspread, its maximum radius and maximum |c_j - c_0| (c_0 = sphere 0's centre).
-__device__ __forceinline__ float stage_tile(const KArgs& a, const Lds& L, int t0, int tn, float kappa, float& rmax,
-                                            float& cspread) {
-  float rmin = INFINITY;
-  rmax = 0.0f;
-  cspread = 0.0f;
+struct Lds {  // the sphere records (global, scalar-loaded) plus the kernel's LDS scratch
+  cf4_ptr P0, P1, P2, P3, S0, S1, W;
+  cf2_ptr P4;
+  float* slots;  // backward wave partials, 2 buffers (LDS)
+  float* misc;   // small LDS scratch
+  __device__ __forceinline__ static float4 v4(f4v v) { return make_float4(v.x, v.y, v.z, v.w); }
+  __device__ __forceinline__ float4 p0(int i) const { return v4(P0[i]); }
+  __device__ __forceinline__ float4 p1(int i) const { return v4(P1[i]); }
+  __device__ __forceinline__ float4 p2(int i) const { return v4(P2[i]); }
+  __device__ __forceinline__ float4 p3(int i) const { return v4(P3[i]); }
+  __device__ __forceinline__ float2 p4(int i) const {
+    const f2v v = P4[i];
+    return make_float2(v.x, v.y);
+  }
+  __device__ __forceinline__ float2 kr(int i) const {
+    const f4v v = P2[i];
+    return make_float2(v.x, v.y);
+  }
+};
+
+__host__ __device__ constexpr size_t lds_bytes() { return (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float) + 64; }
+
+// three-value block reduction (min, max, max) for the record header
+__device__ __forceinline__ void header_reduce(float& rmin, float& rmax, float& spread, float* dst) {
+  __shared__ float red[3][4];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    rmin = fminf(rmin, __shfl_xor(rmin, off));
+    rmax = fmaxf(rmax, __shfl_xor(rmax, off));
+    spread = fmaxf(spread, __shfl_xor(spread, off));
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) {
+    red[0][wave] = rmin;
+    red[1][wave] = rmax;
+    red[2][wave] = spread;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w2 = 1; w2 < 4; ++w2) {
+      red[0][0] = fminf(red[0][0], red[0][w2]);
+      red[1][0] = fmaxf(red[1][0], red[1][w2]);
+      red[2][0] = fmaxf(red[2][0], red[2][w2]);
+    }
+    dst[0] = red[0][0];
+    dst[1] = red[1][0];
+    dst[2] = red[2][0];
+    dst[3] = 0.0f;
+  }
+}
+
+// Records of the call (see Lds), one thread per sphere pair. Each block reduces its pairs'
+// {r_min, r_max, spread} into the header (one block) or its partial (several blocks, then
+// rm_prep_finish).
+__global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a, float4* __restrict__ rec) {
+  const int np = a.Mpad / 2;
+  float4* P0 = rec;
+  float4* P1 = P0 + np;
+  float4* P2 = P1 + np;
+  float4* P3 = P2 + np;
+  float4* S0 = P3 + np;
+  float4* S1 = S0 + np;
+  float4* W = S1 + np;
+  float2* P4 = reinterpret_cast<float2*>(W + np);
+  float* hdr = reinterpret_cast<float*>(P4 + np);
+  const float kappa = a.k * kLog2e, k2 = kappa * kappa;
+  const float kr_first = kappa * a.radius[0];
   const float c0x = a.centers[0], c0y = a.centers[1], c0z = a.centers[2];
-  for (int ip = threadIdx.x; ip < tn / 2; ip += kBlock) {
-    float gx[2], gy[2], gz[2], cc[2], kr[2], rr[2], cr[2], cg[2], cb[2];
+  float rmin = INFINITY, rmax = 0.0f, spread = 0.0f;
+  const int ip = blockIdx.x * 256 + threadIdx.x;
+  if (ip < np) {
+    float gx[2], gy[2], gz[2], cc[2], kr[2], rr[2], cr[2], cg[2], cb[2], w[2], wf[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int j = t0 + 2 * ip + h;
+      const int j = 2 * ip + h;
       if (j < a.M) {
         const float cx = a.centers[3 * j], cy = a.centers[3 * j + 1], cz = a.centers[3 * j + 2];
         const float r = a.radius[j];
@@ -131,65 +196,43 @@ __device__ __forceinline__ float stage_tile(const KArgs& a, const Lds& L, int t0
         cr[h] = a.colors[3 * j];
         cg[h] = a.colors[3 * j + 1];
         cb[h] = a.colors[3 * j + 2];
+        w[h] = fexp2(kr[h]);
+        wf[h] = fexp2(kr[h] - kr_first);
         rmin = fminf(rmin, r);
         rmax = fmaxf(rmax, r);
         const float ex = cx - c0x, ey = cy - c0y, ez = cz - c0z;
-        cspread = fmaxf(cspread, sqrtf(ex * ex + ey * ey + ez * ez));
+        spread = fmaxf(spread, sqrtf(ex * ex + ey * ey + ez * ez));
       } else {
         // padding sphere at c = (kPadCenter, 0, 0): the expansion form (|c|^2) and the direct
         // form of the normal taps (p - c) both see distance ~1e15, so every exp() of its terms
-        // underflows to exactly 0 and all of its gradient terms are exactly 0.
+        // underflows to exactly 0 (its weights are 0) and all of its gradient terms are 0.
         gx[h] = -2.0f * kPadCenter;
         gy[h] = gz[h] = 0.0f;
         cc[h] = kPadCenter * kPadCenter;
-        kr[h] = rr[h] = cr[h] = cg[h] = cb[h] = 0.0f;
+        kr[h] = rr[h] = cr[h] = cg[h] = cb[h] = w[h] = wf[h] = 0.0f;
       }
     }
-    L.P0[ip] = make_float4(gx[0], gx[1], gy[0], gy[1]);
-    L.P1[ip] = make_float4(gz[0], gz[1], cc[0], cc[1]);
-    L.P2[ip] = make_float4(kr[0], kr[1], rr[0], rr[1]);
-    L.P3[ip] = make_float4(cr[0], cr[1], cg[0], cg[1]);
-    L.P4[ip] = make_float2(cb[0], cb[1]);
+    P0[ip] = make_float4(gx[0], gx[1], gy[0], gy[1]);
+    P1[ip] = make_float4(gz[0], gz[1], cc[0], cc[1]);
+    P2[ip] = make_float4(kr[0], kr[1], rr[0], rr[1]);
+    P3[ip] = make_float4(cr[0], cr[1], cg[0], cg[1]);
+    P4[ip] = make_float2(cb[0], cb[1]);
+    S0[ip] = make_float4(k2 * gx[0], k2 * gx[1], k2 * gy[0], k2 * gy[1]);
+    S1[ip] = make_float4(k2 * gz[0], k2 * gz[1], k2 * cc[0], k2 * cc[1]);
+    W[ip] = make_float4(w[0], w[1], wf[0], wf[1]);
   }
-  return rmin;
+  header_reduce(rmin, rmax, spread, gridDim.x == 1 ? hdr : hdr + (size_t)(1 + blockIdx.x) * kRecHeader);
 }
 
-// Weighted march records for spheres [0, Mpad) (M <= 512), written once per call to global
-// memory and read by the march with wave-uniform addresses, i.e. scalar loads into SGPRs that
-// feed the packed VALU ops directly (no LDS broadcast traffic). Per sphere pair ip:
-//   rec[3 ip + 0] = {-2k^2 cx0, -2k^2 cx1, -2k^2 cy0, -2k^2 cy1}
-//   rec[3 ip + 1] = {-2k^2 cz0, -2k^2 cz1, k^2|c0|^2, k^2|c1|^2}
-//   rec[3 ip + 2] = {2^(k r0), 2^(k r1), 2^(k (r0 - r_first)), 2^(k (r1 - r_first))}
-// so sqrt(q') = k rho and a soft-min term is one packed fma: w * 2^(shift - k rho).
-__global__ __launch_bounds__(256) void rm_wrec_kernel(const KArgs a, float4* __restrict__ rec) {
-  const float kappa = a.k * kLog2e;
-  const float k2 = kappa * kappa;
-  const float kr_first = kappa * a.radius[0];
-  for (int ip = threadIdx.x; ip < a.Mpad / 2; ip += 256) {
-    float gx[2], gy[2], gz[2], cc[2], w[2], wf[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int j = 2 * ip + h;
-      if (j < a.M) {
-        const float cx = a.centers[3 * j], cy = a.centers[3 * j + 1], cz = a.centers[3 * j + 2];
-        const float kr = kappa * a.radius[j];
-        gx[h] = -2.0f * k2 * cx;
-        gy[h] = -2.0f * k2 * cy;
-        gz[h] = -2.0f * k2 * cz;
-        cc[h] = k2 * (cx * cx + cy * cy + cz * cz);
-        w[h] = fexp2(kr);
-        wf[h] = fexp2(kr - kr_first);
-      } else {  // padding: q' ~ k^2 1e30 and weight 0, its term is exactly 0
-        gx[h] = -2.0f * k2 * kPadCenter;
-        gy[h] = gz[h] = 0.0f;
-        cc[h] = k2 * kPadCenter * kPadCenter;
-        w[h] = wf[h] = 0.0f;
-      }
-    }
-    rec[3 * ip] = make_float4(gx[0], gx[1], gy[0], gy[1]);
-    rec[3 * ip + 1] = make_float4(gz[0], gz[1], cc[0], cc[1]);
-    rec[3 * ip + 2] = make_float4(w[0], w[1], wf[0], wf[1]);
+__global__ __launch_bounds__(256) void rm_prep_finish(float* __restrict__ hdr, int nprep) {
+  float rmin = INFINITY, rmax = 0.0f, spread = 0.0f;
+  for (int b = threadIdx.x; b < nprep; b += 256) {
+    const float* h = hdr + (size_t)(1 + b) * kRecHeader;
+    rmin = fminf(rmin, h[0]);
+    rmax = fmaxf(rmax, h[1]);
+    spread = fmaxf(spread, h[2]);
   }
+  header_reduce(rmin, rmax, spread, hdr);
 }
 
 // ---- packed helpers --------------------------------------------------------------------------
@@ -229,8 +272,8 @@ __device__ __forceinline__ void lse_point(const float p[3], const Lds& L, int np
     f2 v[8];
 #pragma unroll
     for (int ii = 0; ii < 8; ++ii) {
-      const float4 A = L.P0[i0 + ii], B = L.P1[i0 + ii];
-      const float2 K = reinterpret_cast<const float2*>(L.P2)[2 * (i0 + ii)];
+      const float4 A = L.p0(i0 + ii), B = L.p1(i0 + ii);
+      const float2 K = L.kr(i0 + ii);
       f2 q = qpair(PX, PY, PZ, PP, A, B);
       if constexpr (CLAMP) q = clamp_q(q);
       v[ii] = fma2(sqrt2(q), NK, f2{K.x, K.y});
@@ -263,20 +306,14 @@ __device__ __forceinline__ void lse_point(const float p[3], const Lds& L, int np
 // geometry, term = 2^(k r_j) 2^(-rho'_j) (FIXED = false: shift 0) or 2^(k (r_j - r_0))
 // 2^(rho'_0 - rho'_j) (FIXED: shift v_0 = k r_0 - rho'_0) -- one packed fma per sphere pair
 // instead of the fma + subtract + add of lse_point. Returns the sum; *sh receives rho'_0.
-typedef float f4v __attribute__((ext_vector_type(4)));
-typedef const __attribute__((address_space(4))) f4v* cf4_ptr;  // constant space: scalar loads
-
 template <bool CLAMP, bool FIXED>
-__device__ __forceinline__ float lse_weighted(const float p[3], const float4* rec_g, int npairs, float k2, float& sh) {
-  const cf4_ptr rec = (cf4_ptr)rec_g;  // read-only in this kernel, wave-uniform addresses
+__device__ __forceinline__ float lse_weighted(const float p[3], const Lds& L, int npairs, float k2, float& sh) {
   const f2 PX = sp(p[0]), PY = sp(p[1]), PZ = sp(p[2]), PP = sp(k2 * psq(p)), QMIN = sp(k2 * 1e-6f);
   f2 acc[2] = {sp(0.0f), sp(0.0f)}, SH = sp(0.0f);  // two chains keep the fma latency hidden
   for (int i0 = 0; i0 < npairs; i0 += 8) {
 #pragma unroll
     for (int ii = 0; ii < 8; ++ii) {
-      const f4v a4 = rec[3 * (i0 + ii)], b4 = rec[3 * (i0 + ii) + 1], w4 = rec[3 * (i0 + ii) + 2];
-      const float4 A = make_float4(a4.x, a4.y, a4.z, a4.w), B = make_float4(b4.x, b4.y, b4.z, b4.w),
-                   Wt = make_float4(w4.x, w4.y, w4.z, w4.w);
+      const float4 A = Lds::v4(L.S0[i0 + ii]), B = Lds::v4(L.S1[i0 + ii]), Wt = Lds::v4(L.W[i0 + ii]);
       f2 q = qpair(PX, PY, PZ, PP, A, B);
       if constexpr (CLAMP) q = f2{fmaxf(q.x, QMIN.x), fmaxf(q.y, QMIN.y)};
       const f2 rho = sqrt2(q);
@@ -305,8 +342,8 @@ __device__ __forceinline__ void lse_taps(const float p[3], const Lds& L, int npa
     f2 v[6][4];
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii) {
-      const float4 A = L.P0[i0 + ii], B = L.P1[i0 + ii];
-      const float2 K = reinterpret_cast<const float2*>(L.P2)[2 * (i0 + ii)];
+      const float4 A = L.p0(i0 + ii), B = L.p1(i0 + ii);
+      const float2 K = L.kr(i0 + ii);
       const f2 ex = fma2(HALF, lo(A), PX), ey = fma2(HALF, hi(A), PY), ez = fma2(HALF, lo(B), PZ);
       const f2 Q = fma2(ez, ez, fma2(ey, ey, fma2(ex, ex, E2)));
       f2 q[6] = {fma2(ex, TE, Q), fma2(ex, NTE, Q), fma2(ey, TE, Q), fma2(ey, NTE, Q), fma2(ez, TE, Q),
@@ -356,7 +393,7 @@ __device__ __forceinline__ void shade_sweep(const float p[3], const Lds& L, int 
 #pragma unroll
     for (int ii = 0; ii < 4; ++ii) {
       f2 q, rho;
-      dl[ii] = delta_pair<CLAMP>(PX, PY, PZ, PP, L.P0[i0 + ii], L.P1[i0 + ii], L.P2[i0 + ii], q, rho);
+      dl[ii] = delta_pair<CLAMP>(PX, PY, PZ, PP, L.p0(i0 + ii), L.p1(i0 + ii), L.p2(i0 + ii), q, rho);
     }
     float cmin = fminf(dl[0].x, dl[0].y);
 #pragma unroll
@@ -374,8 +411,8 @@ __device__ __forceinline__ void shade_sweep(const float p[3], const Lds& L, int 
     for (int ii = 0; ii < 4; ++ii) {
       const f2 dd = DN - dl[ii];
       const f2 ew = exp2v(dd * CL), eb = exp2v(dd * KA);
-      const float4 c3 = L.P3[i0 + ii];
-      const float2 c4 = L.P4[i0 + ii];
+      const float4 c3 = L.p3(i0 + ii);
+      const float2 c4 = L.p4(i0 + ii);
       Zw += ew;
       C[0] = fma2(ew, lo(c3), C[0]);
       C[1] = fma2(ew, hi(c3), C[1]);
@@ -559,13 +596,18 @@ template <int MODE, bool CAM>
 __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const KArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   Lds L;
-  const int tile = a.tile;
-  L.P0 = reinterpret_cast<float4*>(smem);
-  L.P1 = L.P0 + tile / 2;
-  L.P2 = L.P1 + tile / 2;
-  L.P3 = L.P2 + tile / 2;
-  L.P4 = reinterpret_cast<float2*>(L.P3 + tile / 2);
-  L.slots = reinterpret_cast<float*>(L.P4 + tile / 2);
+  {
+    const int np = a.Mpad / 2;
+    L.P0 = (cf4_ptr)a.rec_buf;
+    L.P1 = L.P0 + np;
+    L.P2 = L.P1 + np;
+    L.P3 = L.P2 + np;
+    L.S0 = L.P3 + np;
+    L.S1 = L.S0 + np;
+    L.W = L.S1 + np;
+    L.P4 = (cf2_ptr)(L.W + np);
+  }
+  L.slots = reinterpret_cast<float*>(smem);
   L.misc = L.slots + 2 * kWaves * kChunkBwd * 8;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -574,7 +616,6 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   long long ri = a.ray_begin + (valid ? li : 0);  // becomes the ray's row in the [N,3] tensors
 
   const float kappa = a.k * kLog2e, nkappa = -kappa, inv_kappa = 1.0f / kappa;
-  const bool multi = a.Mpad > tile;
 
   // ray (camera.rs:58-87 in camera mode)
   float o[3], d[3];
@@ -589,58 +630,23 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     return;
   }
 
-  // Minimum sphere radius of the scene (single-tile case): with it, a lower bound on the scene
-  // distance proves rho_j = dist_j + r_j >= kSafeRho for every sphere, so max(q, 1e-6) cannot
-  // bind and the sweeps may skip it (exactly the same results). Multi-tile: fast path off.
-  float rmin = -INFINITY;
-  // Block-uniform permissions for the cheaper log-sum-exp shifts of the march (lse_point).
-  bool shift_fixed_ok = false, shift_none_ok = false;
-  if (!multi) {
-    float rmx, spr;
-    float rl = stage_tile(a, L, 0, a.Mpad, kappa, rmx, spr);
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      rl = fminf(rl, __shfl_xor(rl, off));
-      rmx = fmaxf(rmx, __shfl_xor(rmx, off));
-      spr = fmaxf(spr, __shfl_xor(spr, off));
-    }
-    if (lane == 0) {
-      L.misc[wave] = rl;
-      L.misc[kWaves + wave] = rmx;
-      L.misc[2 * kWaves + wave] = spr;
-    }
-    __syncthreads();
-    rmin = L.misc[0];
-    float rmax = L.misc[kWaves], spread = L.misc[2 * kWaves];
-#pragma unroll
-    for (int w = 1; w < kWaves; ++w) {
-      rmin = fminf(rmin, L.misc[w]);
-      rmax = fmaxf(rmax, L.misc[kWaves + w]);
-      spread = fmaxf(spread, L.misc[2 * kWaves + w]);
-    }
-    // |v_j - v_0| = kappa |r_j - r_0 - (rho_j - rho_0)| <= kappa (r_max + |c_j - c_0|); v <= kappa r_max
-    shift_fixed_ok = kappa * (rmax + spread) * 1.001f <= 100.0f;
-    // the weighted form 2^(k r) 2^(-k rho) also needs 2^(-k rho) of the nearest sphere normal:
-    // k rho <= 90 + k r_max <= 120
-    shift_none_ok = kappa * rmax * 1.001f <= (a.wmarch ? 30.0f : 100.0f);
-  }
+  // Scene radius bounds from the record header: with r_min, a lower bound on the scene distance
+  // proves rho_j = dist_j + r_j >= kSafeRho for every sphere, so max(q, 1e-6) cannot bind and
+  // the sweeps may skip it (exactly the same results).
+  const cf1_ptr hdr = (cf1_ptr)(L.P4 + a.Mpad / 2);
+  const float rmin = hdr[0], rmax = hdr[1], spread = hdr[2];
+  // Block-uniform permissions for the cheaper log-sum-exp shifts of the march:
+  // |v_j - v_0| = kappa |r_j - r_0 - (rho_j - rho_0)| <= kappa (r_max + |c_j - c_0|); v <= kappa r_max;
+  // the weighted form 2^(k r) 2^(-k rho) also needs 2^(-k rho) of the nearest sphere normal:
+  // k rho <= 90 + k r_max <= 120
+  const bool shift_fixed_ok = kappa * (rmax + spread) * 1.001f <= 100.0f;
+  const bool shift_none_ok = kappa * rmax * 1.001f <= 30.0f;
   const float kr_first = kappa * a.radius[0];
   // Wave-uniform choice of the clamp-free path from a per-lane lower bound on the distance.
   auto all_safe = [&](float dist_lb) { return __all(dist_lb + rmin >= kSafeRho) != 0; };
 
-  // Visit every sphere tile (restaging LDS only when M exceeds one tile).
-  auto for_tiles = [&](auto&& body) {
-    for (int t0 = 0; t0 < a.Mpad; t0 += tile) {
-      const int tn = min(tile, a.Mpad - t0);
-      if (multi) {
-        __syncthreads();
-        float u0, u1;
-        stage_tile(a, L, t0, tn, kappa, u0, u1);
-        __syncthreads();
-      }
-      body(t0, tn);
-    }
-  };
+  // every sweep visits all sphere pairs in one pass (records are not staged)
+  auto for_tiles = [&](auto&& body) { body(0, a.Mpad); };
   // soft-min scene SDF at one point (scene.rs:60-79 + sdf.rs:30-44); returns D, keeps (m, s)
   auto soft_min = [&](const float p[3], bool fast, float& m, float& s) {
     m = -INFINITY;
@@ -658,14 +664,14 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     const bool none = shift_none_ok && __all(2.0f * fmaxf(Dprev, 0.0f) + a.lse_slack <= 90.0f * inv_kappa);
     float m = none ? 0.0f : -INFINITY, s = 0.0f;
     const bool fixed = !none && shift_fixed_ok && __all(psq(p) <= 1e10f);
-    if (a.wmarch && (none || fixed)) {
+    if (none || fixed) {
       const float k2 = kappa * kappa;
       const int np = a.Mpad / 2;
       float sh;
       if (none) {
-        s = fast ? lse_weighted<false, false>(p, a.wrec, np, k2, sh) : lse_weighted<true, false>(p, a.wrec, np, k2, sh);
+        s = fast ? lse_weighted<false, false>(p, L, np, k2, sh) : lse_weighted<true, false>(p, L, np, k2, sh);
       } else {
-        s = fast ? lse_weighted<false, true>(p, a.wrec, np, k2, sh) : lse_weighted<true, true>(p, a.wrec, np, k2, sh);
+        s = fast ? lse_weighted<false, true>(p, L, np, k2, sh) : lse_weighted<true, true>(p, L, np, k2, sh);
         m = kr_first - sh;
       }
       return -(flog2(fmaxf(s, 1e-30f)) + m) * inv_kappa;
@@ -873,8 +879,8 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
             const int i = (jc + jj) / 2 + u;
-            const float4 A = L.P0[i], B = L.P1[i], R = L.P2[i], C3 = L.P3[i];
-            const float2 C4 = L.P4[i];
+            const float4 A = L.p0(i), B = L.p1(i), R = L.p2(i), C3 = L.p3(i);
+            const float2 C4 = L.p4(i);
             f2 q, rho;
             const f2 dl = delta_pair<CLAMP>(PX, PY, PZ, PP, A, B, R, q, rho);  // bitwise the shade sweep's
             const f2 ir = rcp2(rho);
@@ -937,8 +943,8 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
 #pragma unroll
           for (int u = 0; u < 2; ++u) {
             const int i = (jc + jj) / 2 + u;
-            const float4 A = L.P0[i], B = L.P1[i];
-            const float2 K = reinterpret_cast<const float2*>(L.P2)[2 * i];
+            const float4 A = L.p0(i), B = L.p1(i);
+            const float2 K = L.kr(i);
             f2 q = qpair(PX, PY, PZ, PP, A, B);  // bitwise the reconnect sweep's q
             const f2 qraw = q;
             if constexpr (CLAMP) q = clamp_q(q);
@@ -1292,7 +1298,8 @@ struct rm_context {
   size_t events_used = 0;
   unsigned long long* stats_dev = nullptr;  // escaped-block counter (rm_stats_enable)
   int* esc_flags = nullptr;                 // per-block escape flags, kMaxBlocksPerLaunch ints
-  float4* wrec = nullptr;                   // weighted march records, 256 pairs
+  void* rec = nullptr;                      // sphere records of the current call (rm_prep_kernel)
+  size_t rec_bytes = 0;
   long long stats_blocks = 0;               // ray blocks launched while stats are on
 };
 
@@ -1471,7 +1478,6 @@ int run(rm_context* ctx, const Call& c) {
 
   const int M = c.scene->num_spheres;
   const int Mpad = pad_spheres(M);
-  const int tile = std::min(Mpad, kTileMax);
   a.org = c.org;
   a.dir = c.dir;
   a.centers = c.scene->centers;
@@ -1481,7 +1487,6 @@ int run(rm_context* ctx, const Call& c) {
   a.ambient = c.scene->ambient;
   a.M = M;
   a.Mpad = Mpad;
-  a.tile = tile;
   a.steps = c.march->steps;
   a.k = c.march->smooth_k;
   a.eps = c.march->normal_eps;
@@ -1508,15 +1513,30 @@ int run(rm_context* ctx, const Call& c) {
     for (int i = 0; i < 3; ++i) a.light_fixed[i] = lv[i] / len;
   }
   a.rec = rec_floats(Mpad);
-  // weighted march records (scalar-loaded, see rm_wrec_kernel) for up to 512 spheres
-  a.wmarch = (Mpad <= tile && Mpad <= 512 && n > 0) ? 1 : 0;
-  if (a.wmarch) {
-    if (!ctx->wrec) RM_HIP(ctx, hipMalloc(&ctx->wrec, sizeof(float4) * 3 * 256));
-    hipLaunchKernelGGL(rm_wrec_kernel, dim3(1), dim3(256), 0, ctx->stream, a, ctx->wrec);
+  // sphere records of this call (rm_prep_kernel): read by every sweep through scalar loads
+  if (n > 0) {
+    const int np = Mpad / 2, nprep = (np + 255) / 256;
+    const size_t need = rec_bytes(np, nprep);
+    if (need > ctx->rec_bytes) {
+      if (ctx->rec) {
+        RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        RM_HIP(ctx, hipFree(ctx->rec));
+        ctx->rec = nullptr;
+        ctx->rec_bytes = 0;
+      }
+      if (hipMalloc(&ctx->rec, need) != hipSuccess) return fail(ctx, RM_ERR_OOM, "record buffer (%zu B)", need);
+      ctx->rec_bytes = need;
+    }
+    hipLaunchKernelGGL(rm_prep_kernel, dim3(nprep), dim3(256), 0, ctx->stream, a, (float4*)ctx->rec);
     RM_HIP(ctx, hipGetLastError());
-    a.wrec = ctx->wrec;
+    if (nprep > 1) {
+      float* hdr = reinterpret_cast<float*>((char*)ctx->rec + (size_t)np * (7 * 16 + 8));
+      hipLaunchKernelGGL(rm_prep_finish, dim3(1), dim3(256), 0, ctx->stream, hdr, nprep);
+      RM_HIP(ctx, hipGetLastError());
+    }
+    a.rec_buf = (const float4*)ctx->rec;
   }
-  const size_t lds = lds_bytes(tile);
+  const size_t lds = lds_bytes();
 
   if (has_bwd) {
     if ((rc = ensure_ws(ctx, ws_need(std::max<long long>(n, 1), M))) != RM_OK) return rc;
@@ -1682,11 +1702,11 @@ int rm_stats_collect(rm_context* ctx, int64_t* blocks, int64_t* blocks_skipped, 
 
 void rm_destroy(rm_context* ctx) {
   if (!ctx) return;
-  if (ctx->stats_dev || ctx->esc_flags || ctx->wrec) {
+  if (ctx->stats_dev || ctx->esc_flags || ctx->rec) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stats_dev) (void)hipFree(ctx->stats_dev);
     if (ctx->esc_flags) (void)hipFree(ctx->esc_flags);
-    if (ctx->wrec) (void)hipFree(ctx->wrec);
+    if (ctx->rec) (void)hipFree(ctx->rec);
   }
   for (auto& pr : ctx->events) {
     (void)hipEventDestroy(pr.first);
