@@ -370,6 +370,39 @@ __device__ __forceinline__ void lse_taps(const float p[3], const Lds& L, int npa
   }
 }
 
+// The six taps in weighted form (no shift, see lse_weighted): e' = k (p - c) from the unscaled
+// records, q'_tap = |e'|^2 + (k eps)^2 +- 2 (k eps) e'_a = k^2 q_tap, term = 2^(k r) 2^(-sqrt(q')),
+// one packed fma per tap and pair instead of fma + subtract + add + running max.
+template <bool CLAMP>
+__device__ __forceinline__ void lse_taps_w(const float p[3], const Lds& L, int npairs, float kappa, float eps,
+                                           float (&s)[6]) {
+  const f2 KPX = sp(kappa * p[0]), KPY = sp(kappa * p[1]), KPZ = sp(kappa * p[2]), HK = sp(0.5f * kappa),
+           E2 = sp(kappa * kappa * eps * eps), TE = sp(2.0f * kappa * eps), NTE = sp(-2.0f * kappa * eps),
+           QMIN = sp(kappa * kappa * 1e-6f);
+  f2 acc[6];
+#pragma unroll
+  for (int t = 0; t < 6; ++t) acc[t] = sp(0.0f);
+  for (int i0 = 0; i0 < npairs; i0 += 4) {
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const float4 A = L.p0(i0 + ii), B = L.p1(i0 + ii);
+      const f4v Wt = L.W[i0 + ii];
+      const f2 W = f2{Wt.x, Wt.y};
+      const f2 ex = fma2(HK, lo(A), KPX), ey = fma2(HK, hi(A), KPY), ez = fma2(HK, lo(B), KPZ);
+      const f2 Q = fma2(ez, ez, fma2(ey, ey, fma2(ex, ex, E2)));
+      f2 q[6] = {fma2(ex, TE, Q), fma2(ex, NTE, Q), fma2(ey, TE, Q), fma2(ey, NTE, Q), fma2(ez, TE, Q),
+                 fma2(ez, NTE, Q)};
+#pragma unroll
+      for (int t = 0; t < 6; ++t) {
+        if constexpr (CLAMP) q[t] = f2{fmaxf(q[t].x, QMIN.x), fmaxf(q[t].y, QMIN.y)};
+        acc[t] = fma2(W, exp2v(-sqrt2(q[t])), acc[t]);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 6; ++t) s[t] = acc[t].x + acc[t].y;
+}
+
 // Distances delta_j = rho_j - r_j at p_final for a pair (shade sweep and backward sweep 1 share it).
 template <bool CLAMP>
 __device__ __forceinline__ f2 delta_pair(const f2& PX, const f2& PY, const f2& PZ, const f2& PP, const float4& A,
@@ -747,12 +780,21 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
       s6[q] = 0.0f;
     }
     const float eps = a.eps;
-    if (fast_f)
-      for_tiles([&](int, int tn) { lse_taps<false>(p, L, tn / 2, nkappa, 2.0f * eps, eps * eps, m6, s6); });
-    else
-      for_tiles([&](int, int tn) { lse_taps<true>(p, L, tn / 2, nkappa, 2.0f * eps, eps * eps, m6, s6); });
+    // weighted (unshifted) taps when the hard maximum at every tap is provably >= -90:
+    // d_min(tap) <= d_min(p_a) + |Da| + eps <= 2 max(Da, 0) + ln(M)/k + eps (as in the march)
+    const bool none = shift_none_ok && __all(2.0f * fmaxf(Da, 0.0f) + a.lse_slack + eps <= 90.0f * inv_kappa);
+    if (none) {
+      if (fast_f) lse_taps_w<false>(p, L, a.Mpad / 2, kappa, eps, s6);
+      else lse_taps_w<true>(p, L, a.Mpad / 2, kappa, eps, s6);
 #pragma unroll
-    for (int q = 0; q < 6; ++q) D6[q] = -(flog2(fmaxf(s6[q], 1e-8f)) + m6[q]) * inv_kappa;
+      for (int q = 0; q < 6; ++q) m6[q] = 0.0f;
+    } else if (fast_f) {
+      for_tiles([&](int, int tn) { lse_taps<false>(p, L, tn / 2, nkappa, 2.0f * eps, eps * eps, m6, s6); });
+    } else {
+      for_tiles([&](int, int tn) { lse_taps<true>(p, L, tn / 2, nkappa, 2.0f * eps, eps * eps, m6, s6); });
+    }
+#pragma unroll
+    for (int q = 0; q < 6; ++q) D6[q] = -(flog2(fmaxf(s6[q], 1e-30f)) + m6[q]) * inv_kappa;
     const float nx = D6[0] - D6[1], ny = D6[2] - D6[3], nz = D6[4] - D6[5];
     const float inv_len = frsq(fmaf(nz, nz, fmaf(ny, ny, fmaf(nx, nx, 1e-6f))));
     nrm[0] = nx * inv_len;
