@@ -22,8 +22,9 @@ Synthetic data (no datasets offline): scene seed 0 (BASELINE.md "Synthetic input
 Extra objects on the JSON line:
   roofline      -- the dominant kernel (rm_ray_kernel<train>) timed with hipEvents on its own
                    stream inside the timed region; algorithmic FLOP = 16*(S+10)*M per ray
-                    for the rays whose sphere work actually ran (blocks skipped
-                   by the exact escape test count zero); bound "valu" (fp32 vector);
+                    counted only for sphere sweeps that actually ran (waves
+                   whose rays all escaped stop early, see early_exit; achieved_all_rays counts
+                   every ray); bound "valu" (fp32 vector);
                    traffic = HBM bytes per launch from the committed rocprofv3 PMC summary
                    (profiles/r01_pmc_traffic.json) when present, else null.
   cpu_baseline  -- the oracle's fp32 reference-order C restatement (OpenMP) on a bounded
@@ -158,9 +159,13 @@ def main():
     elapsed = time.perf_counter() - t0
     ctx.timing(False)
     kern_ms, launches = ctx.collect_timing(reset=True)
-    blocks_run, blocks_skipped = ctx.collect_stats(reset=True)
+    st = ctx.collect_stats(reset=True)
     ctx.stats(False)
+    blocks_run, blocks_skipped = st["blocks"], st["blocks_skipped"]
     skipped_frac = blocks_skipped / max(blocks_run, 1)
+    # march steps not run: whole skipped blocks plus waves that left the march early
+    waves_total = max(st["waves"], 1)
+    march_saved_frac = (blocks_skipped * 4 * S + st["steps_saved"]) / (waves_total * S)
     if dist is not None:
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -176,9 +181,14 @@ def main():
     finite = bool(torch.isfinite(model.raw).all().item()) and bool(torch.isfinite(loss).all().item())
 
     # ---- roofline of the dominant kernel -------------------------------------------------
-    # algorithmic work actually executed: escaped blocks run no sphere evaluation at all
+    # algorithmic work actually executed: skipped blocks run no sphere evaluation at all, and a
+    # wave that left the march early skips its remaining march steps and the 10 post-march /
+    # backward sweeps (its outputs and gradient terms are exactly 0)
     flop_per_ray = FLOP_PER_EVAL * (S + 10) * M
-    flops_launch = flop_per_ray * rays_per_rank * (1.0 - skipped_frac)
+    sweeps_total = waves_total * (S + 10)
+    sweeps_saved = blocks_skipped * 4 * (S + 10) + st["steps_saved"] + st["waves_exited"] * 10
+    executed_frac = max(0.0, 1.0 - sweeps_saved / sweeps_total)
+    flops_launch = flop_per_ray * rays_per_rank * executed_frac
     achieved_tf = flops_launch / (kern_avg_ms * 1e-3) / 1e12
     mpad = (M + 31) // 32 * 32
     blocks = (rays_per_rank + 255) // 256
@@ -208,7 +218,8 @@ def main():
         "launches_timed": launches,
         "flop_per_ray": flop_per_ray,
         "rays_per_launch": rays_per_rank,
-        "executed_frac": round(1.0 - skipped_frac, 4),
+        "executed_frac": round(executed_frac, 4),
+        "achieved_all_rays": round(flop_per_ray * rays_per_rank / (kern_avg_ms * 1e-3) / 1e12, 3),
         "hbm": {"algorithmic_bytes_per_launch": alg_bytes,
                 "achieved_GBs": round(alg_bytes / (kern_avg_ms * 1e-3) / 1e9, 2),
                 "peak_GBs": PEAK_HBM_GBS,
@@ -242,6 +253,10 @@ def main():
             "cpu_baseline": cpu,
             "escape_skip": {"enabled": args.skip_escaped == "on", "blocks": blocks_run,
                             "blocks_skipped": blocks_skipped, "skipped_frac": round(skipped_frac, 4)},
+            "early_exit": {"enabled": os.environ.get("RM_NO_EARLY_EXIT") != "1", "waves": st["waves"],
+                           "waves_exited": st["waves_exited"],
+                           "exited_frac": round(st["waves_exited"] / waves_total, 4),
+                           "march_steps_saved_frac": round(march_saved_frac, 4)},
             "finite": finite,
         }
         print(json.dumps(line))

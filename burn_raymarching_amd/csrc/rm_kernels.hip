@@ -59,6 +59,7 @@ struct KArgs {
   float cull_min_d;  // scene distance at which the silhouette mask is exactly 0
   float lse_slack;  // ln(M) / k (rounded up): the hard min exceeds the soft-min by at most this
   unsigned long long* stats;  // nullable: [0] += 1 per escaped (skipped) block
+  float gone_d;               // > 0: waves whose rays all escaped past this distance stop marching
   const int* esc_flags;       // nullable: per-block escape flags of this launch (rm_escape_kernel)
   CamBasis cams[RM_MAX_VIEWS_PER_CALL];
   // activated scene
@@ -129,7 +130,7 @@ struct Lds {  // the sphere records (global, scalar-loaded) plus the kernel's LD
   }
 };
 
-__host__ __device__ constexpr size_t lds_bytes() { return (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float) + 64; }
+__host__ __device__ constexpr size_t lds_bytes() { return (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float) + 256; }
 
 // three-value block reduction (min, max, max) for the record header
 __device__ __forceinline__ void header_reduce(float& rmin, float& rmax, float& spread, float* dst) {
@@ -730,6 +731,9 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   float t = 0.0f;
   float lb = -INFINITY;  // lower bound on the scene distance at the current point
   float Dprev = INFINITY;  // previous march step (none yet)
+  bool dead = false;       // wave-uniform: every ray of the wave has escaped (see below)
+  const float c0x = a.centers[0], c0y = a.centers[1], c0z = a.centers[2];
+  const float gone_r = rmax + spread + a.lse_slack;  // bounding sphere around sphere 0, + soft-min slack
   if (MODE == kBwd && a.t_in != nullptr) {
     t = a.t_in[ri];
   } else {
@@ -747,6 +751,27 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
       if (st == half) __builtin_amdgcn_s_setprio(2);
 #endif
       const float p[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
+      if (a.gone_d > 0.0f) {
+        // Escaped rays: receding from the scene's bounding sphere (c_0, R) with every later
+        // soft-min >= |p - c_0| - R - ln(M)/k >= gone_d (the distance only grows along a
+        // receding ray, so t keeps increasing); the reconnected point and the mask argument
+        // are then >= gone_d too, where sigmoid(-msharp D) (or exp(-10 D^2)) is exactly 0 in
+        // fp32: out = 0 and every gradient term is 0, whatever the remaining steps would give.
+        // A wave whose rays have all escaped stops here. Margins: 1e-5 relative + 1e-3 cover
+        // the fp32 rounding of the march at any |p|.
+        const float ex = p[0] - c0x, ey = p[1] - c0y, ez = p[2] - c0z;
+        const float dist = sqrtf(fmaf(ez, ez, fmaf(ey, ey, ex * ex)));
+        const bool gone = fmaf(ez, d[2], fmaf(ey, d[1], ex * d[0])) >= 0.0f &&
+                          dist * (1.0f - 1e-5f) - gone_r - 1e-3f >= a.gone_d;
+        if (__all(gone || !valid)) {
+          dead = true;
+          if (a.stats != nullptr && lane == 0) {
+            atomicAdd(a.stats + 1, 1ull);
+            atomicAdd(a.stats + 2, (unsigned long long)(a.steps - st));
+          }
+          break;
+        }
+      }
       const float D = soft_min_march(p, all_safe(lb), Dprev);
       t += D;
       // next point: hard min >= soft-min D here, moved by |D|
@@ -759,93 +784,102 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
 #endif
   if ((MODE == kFwd || MODE == kRender) && a.t_out != nullptr && valid) a.t_out[ri] = t;
 
-  // ---- reconnect: t_final = t + sdf(p_approx) (renderer_diff.rs:30-39); renderer.rs has none
-  const float pa[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
-  float mA = 0.0f, sA = 1.0f, Da = 0.0f;
-  const bool fast_a = all_safe(lb);
-  if constexpr (MODE != kRender) Da = soft_min(pa, fast_a, mA, sA);
-  const float tf = t + Da;
-  const float p[3] = {fmaf(d[0], tf, o[0]), fmaf(d[1], tf, o[1]), fmaf(d[2], tf, o[2])};
-  // p_final is |Da| from p_approx; the taps another eps away
-  const bool fast_f = MODE == kRender ? all_safe(lb - a.eps) : all_safe(-mA * inv_kappa - fabsf(Da) - a.eps);
-
-  // ---- detached 6-tap normal (scene.rs:81-128)
-  float nrm[3];
-  float D6[6];
-  {
-    float m6[6], s6[6];
-#pragma unroll
-    for (int q = 0; q < 6; ++q) {
-      m6[q] = -INFINITY;
-      s6[q] = 0.0f;
-    }
-    const float eps = a.eps;
-    // weighted (unshifted) taps when the hard maximum at every tap is provably >= -90:
-    // d_min(tap) <= d_min(p_a) + |Da| + eps <= 2 max(Da, 0) + ln(M)/k + eps (as in the march)
-    const bool none = shift_none_ok && __all(2.0f * fmaxf(Da, 0.0f) + a.lse_slack + eps <= 90.0f * inv_kappa);
-    if (none) {
-      if (fast_f) lse_taps_w<false>(p, L, a.Mpad / 2, kappa, eps, s6);
-      else lse_taps_w<true>(p, L, a.Mpad / 2, kappa, eps, s6);
-#pragma unroll
-      for (int q = 0; q < 6; ++q) m6[q] = 0.0f;
-    } else if (fast_f) {
-      for_tiles([&](int, int tn) { lse_taps<false>(p, L, tn / 2, nkappa, 2.0f * eps, eps * eps, m6, s6); });
-    } else {
-      for_tiles([&](int, int tn) { lse_taps<true>(p, L, tn / 2, nkappa, 2.0f * eps, eps * eps, m6, s6); });
-    }
-#pragma unroll
-    for (int q = 0; q < 6; ++q) D6[q] = -(flog2(fmaxf(s6[q], 1e-30f)) + m6[q]) * inv_kappa;
-    const float nx = D6[0] - D6[1], ny = D6[2] - D6[3], nz = D6[4] - D6[5];
-    const float inv_len = frsq(fmaf(nz, nz, fmaf(ny, ny, fmaf(nx, nx, 1e-6f))));
-    nrm[0] = nx * inv_len;
-    nrm[1] = ny * inv_len;
-    nrm[2] = nz * inv_len;
-  }
-
-  // ---- lighting (renderer_diff.rs:48-62; renderer.rs:27-40 in kRender)
-  float ldn[3], amb = 0.0f;
-  if constexpr (MODE == kRender) {
-    ldn[0] = a.light_fixed[0];
-    ldn[1] = a.light_fixed[1];
-    ldn[2] = a.light_fixed[2];
-  } else {
-    const float ld0 = a.light_dir[0], ld1 = a.light_dir[1], ld2 = a.light_dir[2];
-    amb = a.ambient[0];
-    const float ldlen = sqrtf(ld0 * ld0 + ld1 * ld1 + ld2 * ld2);
-    ldn[0] = ld0 / ldlen;
-    ldn[1] = ld1 / ldlen;
-    ldn[2] = ld2 / ldlen;
-  }
-  const float sdot = fmaf(nrm[2], ldn[2], fmaf(nrm[1], ldn[1], nrm[0] * ldn[0]));
-  const float dif = fmaxf(sdot, 0.0f);
-  const float Lgt = MODE == kRender ? dif + 0.1f : fmaf(dif, 1.0f - amb, amb);
-
-  // ---- colour softmax + mask (renderer_diff.rs:64-90)
+  // Post-march forward state. A wave whose rays have all escaped (see the march loop) keeps
+  // the defaults: out = mix L mu = 0 with mu = 0, and every backward seed is 0.
   const float c10l = a.csharp * kLog2e;
-  float dmin = INFINITY;
-  f2 Zw2 = sp(0.0f), Zb2 = sp(0.0f), C2[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
-  if (fast_f)
-    for_tiles([&](int, int tn) { shade_sweep<false>(p, L, tn / 2, c10l, kappa, dmin, Zw2, C2, Zb2); });
-  else
-    for_tiles([&](int, int tn) { shade_sweep<true>(p, L, tn / 2, c10l, kappa, dmin, Zw2, C2, Zb2); });
-  const float Zw = Zw2.x + Zw2.y, Zb = Zb2.x + Zb2.y;
-  const float Df = dmin - flog2(fmaxf(Zb, 1e-8f)) * inv_kappa;
-  float mix[3], mu;
-  if constexpr (MODE == kRender) {
-    // renderer.rs:52-71: raw exp(-10 d) weights, mixed = sum(col w) / (sum(w) + 1e-5); the sums
-    // above are shifted by exp(10 dmin), undone here; mask = exp(-10 D^2) (renderer.rs:77)
-    const float e = fexp2(-c10l * dmin);
-    const float den = Zw * e + 1e-5f;
-    mix[0] = (C2[0].x + C2[0].y) * e / den;
-    mix[1] = (C2[1].x + C2[1].y) * e / den;
-    mix[2] = (C2[2].x + C2[2].y) * e / den;
-    mu = fexp2(-10.0f * kLog2e * Df * Df);
-  } else {
-    const float invZw0 = frcp(Zw);
-    mix[0] = (C2[0].x + C2[0].y) * invZw0;
-    mix[1] = (C2[1].x + C2[1].y) * invZw0;
-    mix[2] = (C2[2].x + C2[2].y) * invZw0;
-    mu = frcp(1.0f + fexp2(a.msharp * kLog2e * Df));  // sigmoid(-msharp * D)
+  float pa[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
+  float p[3] = {pa[0], pa[1], pa[2]};
+  float mA = 0.0f, sA = 1.0f, Da = 0.0f, tf = t;
+  bool fast_a = false, fast_f = false;
+  float nrm[3] = {0.0f, 0.0f, 0.0f}, D6[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+  float amb = 0.0f, sdot = 0.0f, dif = 0.0f, Lgt = 0.0f;
+  float dmin = 0.0f, Zw = 1.0f, Zb = 1.0f, Df = 0.0f, mix[3] = {0.0f, 0.0f, 0.0f}, mu = 0.0f;
+  if (!dead) {
+    // ---- reconnect: t_final = t + sdf(p_approx) (renderer_diff.rs:30-39); renderer.rs has none
+    fast_a = all_safe(lb);
+    if constexpr (MODE != kRender) Da = soft_min(pa, fast_a, mA, sA);
+    tf = t + Da;
+    p[0] = fmaf(d[0], tf, o[0]);
+    p[1] = fmaf(d[1], tf, o[1]);
+    p[2] = fmaf(d[2], tf, o[2]);
+    // p_final is |Da| from p_approx; the taps another eps away
+    fast_f = MODE == kRender ? all_safe(lb - a.eps) : all_safe(-mA * inv_kappa - fabsf(Da) - a.eps);
+
+    // ---- detached 6-tap normal (scene.rs:81-128)
+    {
+      float m6[6], s6[6];
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        m6[q] = -INFINITY;
+        s6[q] = 0.0f;
+      }
+      const float eps = a.eps;
+      // weighted (unshifted) taps when the hard maximum at every tap is provably >= -90:
+      // d_min(tap) <= d_min(p_a) + |Da| + eps <= 2 max(Da, 0) + ln(M)/k + eps (as in the march)
+      const bool none = shift_none_ok && __all(2.0f * fmaxf(Da, 0.0f) + a.lse_slack + eps <= 90.0f * inv_kappa);
+      if (none) {
+        if (fast_f) lse_taps_w<false>(p, L, a.Mpad / 2, kappa, eps, s6);
+        else lse_taps_w<true>(p, L, a.Mpad / 2, kappa, eps, s6);
+#pragma unroll
+        for (int q = 0; q < 6; ++q) m6[q] = 0.0f;
+      } else if (fast_f) {
+        for_tiles([&](int, int tn) { lse_taps<false>(p, L, tn / 2, nkappa, 2.0f * eps, eps * eps, m6, s6); });
+      } else {
+        for_tiles([&](int, int tn) { lse_taps<true>(p, L, tn / 2, nkappa, 2.0f * eps, eps * eps, m6, s6); });
+      }
+#pragma unroll
+      for (int q = 0; q < 6; ++q) D6[q] = -(flog2(fmaxf(s6[q], 1e-30f)) + m6[q]) * inv_kappa;
+      const float nx = D6[0] - D6[1], ny = D6[2] - D6[3], nz = D6[4] - D6[5];
+      const float inv_len = frsq(fmaf(nz, nz, fmaf(ny, ny, fmaf(nx, nx, 1e-6f))));
+      nrm[0] = nx * inv_len;
+      nrm[1] = ny * inv_len;
+      nrm[2] = nz * inv_len;
+    }
+
+    // ---- lighting (renderer_diff.rs:48-62; renderer.rs:27-40 in kRender)
+    float ldn[3];
+    if constexpr (MODE == kRender) {
+      ldn[0] = a.light_fixed[0];
+      ldn[1] = a.light_fixed[1];
+      ldn[2] = a.light_fixed[2];
+    } else {
+      const float ld0 = a.light_dir[0], ld1 = a.light_dir[1], ld2 = a.light_dir[2];
+      amb = a.ambient[0];
+      const float ldlen = sqrtf(ld0 * ld0 + ld1 * ld1 + ld2 * ld2);
+      ldn[0] = ld0 / ldlen;
+      ldn[1] = ld1 / ldlen;
+      ldn[2] = ld2 / ldlen;
+    }
+    sdot = fmaf(nrm[2], ldn[2], fmaf(nrm[1], ldn[1], nrm[0] * ldn[0]));
+    dif = fmaxf(sdot, 0.0f);
+    Lgt = MODE == kRender ? dif + 0.1f : fmaf(dif, 1.0f - amb, amb);
+
+    // ---- colour softmax + mask (renderer_diff.rs:64-90)
+    dmin = INFINITY;
+    f2 Zw2 = sp(0.0f), Zb2 = sp(0.0f), C2[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
+    if (fast_f)
+      for_tiles([&](int, int tn) { shade_sweep<false>(p, L, tn / 2, c10l, kappa, dmin, Zw2, C2, Zb2); });
+    else
+      for_tiles([&](int, int tn) { shade_sweep<true>(p, L, tn / 2, c10l, kappa, dmin, Zw2, C2, Zb2); });
+    Zw = Zw2.x + Zw2.y;
+    Zb = Zb2.x + Zb2.y;
+    Df = dmin - flog2(fmaxf(Zb, 1e-8f)) * inv_kappa;
+    if constexpr (MODE == kRender) {
+      // renderer.rs:52-71: raw exp(-10 d) weights, mixed = sum(col w) / (sum(w) + 1e-5); the sums
+      // above are shifted by exp(10 dmin), undone here; mask = exp(-10 D^2) (renderer.rs:77)
+      const float e = fexp2(-c10l * dmin);
+      const float den = Zw * e + 1e-5f;
+      mix[0] = (C2[0].x + C2[0].y) * e / den;
+      mix[1] = (C2[1].x + C2[1].y) * e / den;
+      mix[2] = (C2[2].x + C2[2].y) * e / den;
+      mu = fexp2(-10.0f * kLog2e * Df * Df);
+    } else {
+      const float invZw0 = frcp(Zw);
+      mix[0] = (C2[0].x + C2[0].y) * invZw0;
+      mix[1] = (C2[1].x + C2[1].y) * invZw0;
+      mix[2] = (C2[2].x + C2[2].y) * invZw0;
+      mu = frcp(1.0f + fexp2(a.msharp * kLog2e * Df));  // sigmoid(-msharp * D)
+    }
   }
   const float invZw = frcp(Zw);
   const float scale = Lgt * mu;
@@ -906,6 +940,50 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   float* slots = L.slots;
   int chunk_ctr = 0;
 
+  // ---- per-ray scalars (light before the projection, ambient, loss) and the early-exit
+  // hand-off: every wave publishes its scalar sums and whether it left the march early; after
+  // this barrier such waves end (an ended wave no longer counts in s_barrier) and the others
+  // run the backward sweeps and combine only their own partials. The escaped waves' terms are
+  // exactly 0, so the record is the one the full computation would write.
+  int* wflag = reinterpret_cast<int*>(L.misc);  // [kWaves]
+  float* wscal = L.misc + 8;                     // [kWaves][8]
+  {
+    const float vals[8] = {gell[0], gell[1], gell[2], gamb, loss, 0.0f, 0.0f, 0.0f};
+    const float red = wave_reduce8(vals, lane);
+    if ((lane & 7) == 7) wscal[wave * 8 + (lane >> 3)] = red;
+    if (lane == 0) wflag[wave] = dead ? 1 : 0;
+  }
+  __syncthreads();
+  int alive = 0;
+#pragma unroll
+  for (int w = 0; w < kWaves; ++w) alive |= wflag[w] ? 0 : (1 << w);
+  if (dead) {
+    if (alive == 0 && wave == 0) {  // the whole block escaped: zero record + scalar totals
+      for (long long e = lane; e < (long long)a.Mpad * 12; e += 64) rec[e] = 0.0f;
+      if (lane < 8) {
+        float acc = wscal[lane];
+#pragma unroll
+        for (int w = 1; w < kWaves; ++w) acc += wscal[w * 8 + lane];
+        rec[(long long)a.Mpad * 12 + lane] = acc;
+      }
+    }
+    return;
+  }
+  const int arank = __popc(alive & ((1 << wave) - 1));
+  const int atid = arank * 64 + lane, astride = __popc(alive) * 64;
+  // sum of the live waves' slots, in wave order (the order the all-alive case uses)
+  auto live_sum = [&](const float* s0, int stride) {
+    float acc = 0.0f;
+    bool first = true;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w)
+      if (alive & (1 << w)) {
+        acc = first ? s0[w * stride] : acc + s0[w * stride];
+        first = false;
+      }
+    return acc;
+  };
+
   // ---- backward sweep 1 at p_final: colour softmax + mask soft-min + p_final(t_final)
   f2 GP[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
   {
@@ -954,13 +1032,7 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
           }
         }
         __syncthreads();
-        for (int e = tid; e < kChunkBwd * 8; e += kBlock) {
-          const float* s0 = sb + e;
-          float acc = s0[0];
-#pragma unroll
-          for (int w = 1; w < kWaves; ++w) acc += s0[w * kChunkBwd * 8];
-          rec[(long long)(t0 + jc) * 8 + e] = acc;
-        }
+        for (int e = atid; e < kChunkBwd * 8; e += astride) rec[(long long)(t0 + jc) * 8 + e] = live_sum(sb + e, kChunkBwd * 8);
       }
     };
     if (fast_f)
@@ -1010,13 +1082,8 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
           }
         }
         __syncthreads();
-        for (int e = tid; e < kChunkBwd * 4; e += kBlock) {
-          const float* s0 = sb + e;
-          float acc = s0[0];
-#pragma unroll
-          for (int w = 1; w < kWaves; ++w) acc += s0[w * kChunkBwd * 4];
-          rec[(long long)a.Mpad * 8 + (long long)(t0 + jc) * 4 + e] = acc;
-        }
+        for (int e = atid; e < kChunkBwd * 4; e += astride)
+          rec[(long long)a.Mpad * 8 + (long long)(t0 + jc) * 4 + e] = live_sum(sb + e, kChunkBwd * 4);
       }
     };
     if (fast_a)
@@ -1026,18 +1093,12 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   }
   __syncthreads();
 
-  // ---- per-ray scalars: light (pre-projection), ambient, loss
-  {
-    const float vals[8] = {gell[0], gell[1], gell[2], gamb, loss, 0.0f, 0.0f, 0.0f};
-    const float red = wave_reduce8(vals, lane);
-    if ((lane & 7) == 7) slots[wave * 8 + (lane >> 3)] = red;
-    __syncthreads();
-    if (tid < 8) {
-      float acc = slots[tid];
+  // ---- per-ray scalar totals of the block (published before the sweeps)
+  if (arank == 0 && lane < 8) {
+    float acc = wscal[lane];
 #pragma unroll
-      for (int w = 1; w < kWaves; ++w) acc += slots[w * 8 + tid];
-      rec[(long long)a.Mpad * 12 + tid] = acc;
-    }
+    for (int w = 1; w < kWaves; ++w) acc += wscal[w * 8 + lane];
+    rec[(long long)a.Mpad * 12 + lane] = acc;
   }
 }
 
@@ -1548,6 +1609,13 @@ int run(rm_context* ctx, const Call& c) {
   a.cull = ((c.march->flags & RM_MARCH_SKIP_ESCAPED) != 0 && mask_vanishes && !c.t_out && !c.dbg) ? 1 : 0;
   a.cull_min_d = c.mode == kRender ? 50.0f : std::max(50.0f, 160.0f / (a.msharp * 1.44269504f));
   a.lse_slack = (float)(std::log((double)M) / (double)a.k * (1.0 + 1e-6)) + 1e-7f;
+  // Escaped-ray early exit: the mask must be exactly 0 at distance gone_d -- exp2 of
+  // msharp log2(e) D overflows past 128 (use 170); exp(-10 D^2) underflows long before 8.
+  a.gone_d = 0.0f;
+  if ((c.march->flags & RM_MARCH_NO_EARLY_EXIT) == 0 && !c.t_out && !c.dbg) {
+    if (c.mode == kRender) a.gone_d = 8.0f;
+    else if (a.msharp > 0.0f) a.gone_d = std::max(8.0f, 170.0f / (a.msharp * 1.44269504f));
+  }
   if (!a.cull && (c.march->flags & RM_MARCH_TILE16) == 0) a.tiling = 0;
   if (c.mode == kRender) {  // renderer.rs:27-32, normalised in f32 on the host like the reference
     const float lv[3] = {-0.5f, 0.5f, -1.0f};
@@ -1716,8 +1784,8 @@ int rm_timing_collect(rm_context* ctx, double* total_ms, int64_t* launches, int3
 int rm_stats_enable(rm_context* ctx, int32_t enable) {
   if (!ctx) return RM_ERR_INVALID_ARG;
   if (enable && !ctx->stats_dev) {
-    RM_HIP(ctx, hipMalloc(&ctx->stats_dev, sizeof(unsigned long long)));
-    RM_HIP(ctx, hipMemsetAsync(ctx->stats_dev, 0, sizeof(unsigned long long), ctx->stream));
+    RM_HIP(ctx, hipMalloc(&ctx->stats_dev, 4 * sizeof(unsigned long long)));
+    RM_HIP(ctx, hipMemsetAsync(ctx->stats_dev, 0, 4 * sizeof(unsigned long long), ctx->stream));
     ctx->stats_blocks = 0;
   } else if (!enable && ctx->stats_dev) {
     RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -1727,14 +1795,17 @@ int rm_stats_enable(rm_context* ctx, int32_t enable) {
   return RM_OK;
 }
 
-int rm_stats_collect(rm_context* ctx, int64_t* blocks, int64_t* blocks_skipped, int32_t reset) {
-  if (!ctx || !blocks || !blocks_skipped) return RM_ERR_INVALID_ARG;
+int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset) {
+  if (!ctx || !out) return RM_ERR_INVALID_ARG;
   if (!ctx->stats_dev) return fail(ctx, RM_ERR_INVALID_ARG, "stats are not enabled");
-  unsigned long long v = 0;
-  RM_HIP(ctx, hipMemcpyAsync(&v, ctx->stats_dev, sizeof v, hipMemcpyDeviceToHost, ctx->stream));
+  unsigned long long v[4];
+  RM_HIP(ctx, hipMemcpyAsync(v, ctx->stats_dev, sizeof v, hipMemcpyDeviceToHost, ctx->stream));
   RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  *blocks = ctx->stats_blocks;
-  *blocks_skipped = (int64_t)v;
+  out->blocks = ctx->stats_blocks;
+  out->blocks_skipped = (int64_t)v[0];
+  out->waves = ctx->stats_blocks * kWaves;
+  out->waves_exited = (int64_t)v[1];
+  out->steps_saved = (int64_t)v[2];
   if (reset) {
     RM_HIP(ctx, hipMemsetAsync(ctx->stats_dev, 0, sizeof v, ctx->stream));
     ctx->stats_blocks = 0;

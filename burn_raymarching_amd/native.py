@@ -35,6 +35,12 @@ class RmMarch(ctypes.Structure):
 
 RM_MARCH_SKIP_ESCAPED = 1
 RM_MARCH_TILE16 = 2
+RM_MARCH_NO_EARLY_EXIT = 4
+
+
+class RmStats(ctypes.Structure):
+    _fields_ = [("blocks", _I64), ("blocks_skipped", _I64), ("waves", _I64), ("waves_exited", _I64),
+                ("steps_saved", _I64)]
 
 
 class RmCamera(ctypes.Structure):
@@ -75,7 +81,7 @@ SIGNATURES = {
     "rm_timing_enable": (ctypes.c_int, [_P, _I32]),
     "rm_timing_collect": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64), _I32]),
     "rm_stats_enable": (ctypes.c_int, [_P, _I32]),
-    "rm_stats_collect": (ctypes.c_int, [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64), _I32]),
+    "rm_stats_collect": (ctypes.c_int, [_P, ctypes.POINTER(RmStats), _I32]),
     "rm_scene_activate": (ctypes.c_int, [_P, _P, _I32, _P]),
     "rm_scene_from_packed": (None, [_P, _I32, ctypes.POINTER(RmScene)]),
     "rm_grads_from_packed": (None, [_P, _I32, ctypes.POINTER(RmGrads)]),
@@ -151,12 +157,11 @@ class Context:
     def stats(self, enable: bool = True):
         self.check(self._lib.rm_stats_enable(self.handle, 1 if enable else 0), "rm_stats_enable")
 
-    def collect_stats(self, reset: bool = True):
-        """(ray blocks launched, blocks skipped as escaping) since the last reset."""
-        b, s = _I64(), _I64()
-        self.check(self._lib.rm_stats_collect(self.handle, ctypes.byref(b), ctypes.byref(s), 1 if reset else 0),
-                   "rm_stats_collect")
-        return b.value, s.value
+    def collect_stats(self, reset: bool = True) -> dict:
+        """rm_stats since the last reset: blocks, blocks_skipped, waves, waves_exited, steps_saved."""
+        st = RmStats()
+        self.check(self._lib.rm_stats_collect(self.handle, ctypes.byref(st), 1 if reset else 0), "rm_stats_collect")
+        return {name: getattr(st, name) for name, _ in RmStats._fields_}
 
     def close(self):
         if getattr(self, "handle", None) is not None and self.handle.value:
@@ -173,11 +178,14 @@ class Context:
 def march_params(steps=40, smooth_k=32.0, normal_eps=1e-4, color_sharpness=10.0, mask_sharpness=15.0,
                  skip_escaped=None) -> RmMarch:
     """rm_march; skip_escaped None = the process default (env RM_SKIP_ESCAPED=1, else off);
-    env RM_TILE16=1 adds RM_MARCH_TILE16 (camera-mode pixel order of the skip, for A/B tests)."""
+    env RM_TILE16=1 adds RM_MARCH_TILE16 (camera-mode pixel order of the skip, for A/B tests),
+    env RM_NO_EARLY_EXIT=1 adds RM_MARCH_NO_EARLY_EXIT (A/B tests)."""
     if skip_escaped is None:
         skip_escaped = os.environ.get("RM_SKIP_ESCAPED", "0") == "1"
     flags = (RM_MARCH_SKIP_ESCAPED if skip_escaped else 0) | (RM_MARCH_TILE16 if os.environ.get("RM_TILE16") == "1"
                                                               else 0)
+    if os.environ.get("RM_NO_EARLY_EXIT") == "1":
+        flags |= RM_MARCH_NO_EARLY_EXIT
     return RmMarch(int(steps), float(smooth_k), float(normal_eps), float(color_sharpness), float(mask_sharpness),
                    flags)
 

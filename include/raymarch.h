@@ -82,6 +82,11 @@ typedef struct rm_march {
  * (implied by RM_MARCH_SKIP_ESCAPED; needs width and height multiples of 16). Changes only the
  * summation order of the gradients. */
 #define RM_MARCH_TILE16 2
+/* Disable the escaped-ray early exit: by default a wave stops marching once all its rays
+ * recede from the scene's bounding sphere at a distance where the silhouette mask is exactly
+ * 0 in fp32 (their outputs and gradient terms are then exactly 0, as the full computation
+ * gives). Set for A/B timing; t_march and debug outputs disable it automatically. */
+#define RM_MARCH_NO_EARLY_EXIT 4
 
 /* Pinhole LookAt camera, camera.rs:30-37. Rays are generated in-kernel exactly as
  * create_camera_rays (camera.rs:41-87): rows y then x, u = x/W*2-1, v = -(y/H*2-1). */
@@ -189,10 +194,18 @@ int rm_timing_collect(rm_context* ctx, double* total_ms, int64_t* launches, int3
 
 /* ---- work statistics -------------------------------------------------------- */
 /* rm_stats_enable(ctx, 1): count, for every later per-ray launch, the ray blocks (256 rays)
- * launched and those skipped by RM_MARCH_SKIP_ESCAPED. rm_stats_collect synchronises the
- * stream; reset != 0 clears both counters. */
+ * launched, those skipped whole by RM_MARCH_SKIP_ESCAPED, and the waves (64 rays) that left
+ * the march early because all their rays escaped, with the march steps they saved.
+ * rm_stats_collect synchronises the stream; reset != 0 clears the counters. */
+typedef struct rm_stats {
+  int64_t blocks;          /* ray blocks launched */
+  int64_t blocks_skipped;  /* blocks skipped by RM_MARCH_SKIP_ESCAPED */
+  int64_t waves;           /* waves launched (4 per block) */
+  int64_t waves_exited;    /* waves that stopped marching early (all rays escaped) */
+  int64_t steps_saved;     /* march steps those waves did not run */
+} rm_stats;
 int rm_stats_enable(rm_context* ctx, int32_t enable);
-int rm_stats_collect(rm_context* ctx, int64_t* blocks, int64_t* blocks_skipped, int32_t reset);
+int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset);
 
 /* ---- model helpers: SceneModel activations, compute_loss penalties, Adam ---- */
 /* Packed parameter layout used by the helpers (raw Param tensors or their grads):

@@ -1,0 +1,86 @@
+"""Escaped-ray early exit (default; RM_MARCH_NO_EARLY_EXIT / env RM_NO_EARLY_EXIT=1 turns it
+off): a wave whose rays all recede from the scene at a distance where the mask is exactly 0
+stops marching and contributes out = 0 and zero gradient terms. With the exit on and off the
+image, the train-step loss and every gradient are equal (==), and the counters show exits."""
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
+
+
+@pytest.fixture(scope="module")
+def mods():
+    import torch
+    from burn_raymarching_amd import model, render
+    torch.cuda.init()
+    return torch, model, render
+
+
+def _both(monkeypatch, fn):
+    monkeypatch.setenv("RM_NO_EARLY_EXIT", "1")
+    full = fn()
+    monkeypatch.setenv("RM_NO_EARLY_EXIT", "0")
+    fast = fn()
+    return full, fast
+
+
+def _stats(render, fn):
+    ctx = render.context()
+    ctx.stats(True)
+    ctx.collect_stats(reset=True)
+    fn()
+    st = ctx.collect_stats(reset=True)
+    ctx.stats(False)
+    return st
+
+
+@pytest.mark.parametrize("m,k,steps,size,msharp", [(64, 32.0, 32, 128, 15.0), (256, 32.0, 32, 96, 15.0),
+                                                   (40, 5.0, 40, 64, 15.0), (300, 32.0, 40, 80, 15.0),
+                                                   (64, 32.0, 32, 64, 4.0)])
+def test_train_step_identical_with_early_exit(mods, monkeypatch, m, k, steps, size, msharp):
+    torch, model, render = mods
+    sc = model.scene_tensors(model.synthetic_scene(m, 3), "cuda")
+    cams = model.ring_cameras(10)[:2]
+    tgt = render.render_diff_camera(cams, size, size, model.scene_tensors(model.synthetic_scene(m, 4), "cuda"),
+                                    32.0, steps)
+    from burn_raymarching_amd import native
+
+    def run():
+        out = torch.empty_like(tgt)
+        march = native.march_params(steps, k, mask_sharpness=msharp)
+        loss, g, _ = render.train_step_camera(cams, size, size, tgt, sc, k, 0.3, steps, out=out, march=march)
+        torch.cuda.synchronize()
+        return loss.clone(), {key: v.clone() for key, v in g.items()}, out
+
+    (l0, g0, o0), (l1, g1, o1) = _both(monkeypatch, run)
+    assert torch.equal(o0, o1)
+    assert torch.equal(l0, l1)
+    for key in g0:
+        assert torch.equal(g0[key], g1[key]), key
+    monkeypatch.setenv("RM_NO_EARLY_EXIT", "0")
+    st = _stats(render, run)
+    assert st["waves"] == 2 * size * size // 64
+    if k == 32.0:
+        assert st["waves_exited"] > 0 and st["steps_saved"] > 0
+
+
+def test_forward_backward_and_render_identical(mods, monkeypatch):
+    torch, model, render = mods
+    sc_np = model.synthetic_scene(128, 7)
+    sc = model.scene_tensors(sc_np, "cuda")
+    cams = model.ring_cameras(10)[3:6]
+    out0, out1 = _both(monkeypatch, lambda: render.render_diff_camera(cams, 64, 64, sc, 32.0, 32))
+    assert torch.equal(out0, out1)
+    g = torch.randn((3 * 4096, 3), device="cuda", generator=torch.Generator("cuda").manual_seed(0))
+    b0, b1 = _both(monkeypatch, lambda: render.render_diff_backward_camera(cams, 64, 64, sc, 32.0, g, 32))
+    for key in b0:
+        assert torch.equal(b0[key], b1[key]), key
+    c, col, r = (torch.tensor(sc_np[k2], device="cuda") for k2 in ("centers", "colors", "radius"))
+    r0, r1 = _both(monkeypatch, lambda: render.render_camera(cams, 64, 64, c, col, r))
+    assert torch.equal(r0, r1)
+    # with return_t the full march is needed for every ray: no early exit
+    monkeypatch.setenv("RM_NO_EARLY_EXIT", "0")
+    st = _stats(render, lambda: render.render_diff_camera(cams, 64, 64, sc, 32.0, 32, return_t=True))
+    assert st["waves_exited"] == 0

@@ -39,9 +39,9 @@ def _skipped(render, fn):
     ctx.stats(True)
     ctx.collect_stats(reset=True)
     fn()
-    blocks, skipped = ctx.collect_stats(reset=True)
+    st = ctx.collect_stats(reset=True)
     ctx.stats(False)
-    return blocks, skipped
+    return st["blocks"], st["blocks_skipped"]
 
 
 @pytest.mark.parametrize("m,k,steps,size", [(64, 32.0, 32, 128), (256, 32.0, 32, 96), (40, 5.0, 16, 64),
