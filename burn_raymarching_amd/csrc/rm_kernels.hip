@@ -1564,8 +1564,8 @@ int run(rm_context* ctx, const Call& c) {
       if ((rc = make_basis(ctx, c.cams[v], c.W, c.H, a.cams[v])) != RM_OK) return rc;
     a.width = c.W;
     a.height = c.H;
-    // Row order measures fastest for full work (314 vs 304 Mrays/s with 16x16 tiles at the
-    // metric config); compact 16x16 tiles only pay when whole blocks can be skipped.
+    // Compact 16x16 tiles per block (8x8 per wave): more waves whose rays all miss the scene
+    // leave the march early (68 % vs 62 % of waves at the metric view, +3-4 %).
     a.tiling = (c.W % 16 == 0 && c.H % 16 == 0) ? 2 : 0;
     a.num_views = c.views;
   } else {
@@ -1616,7 +1616,7 @@ int run(rm_context* ctx, const Call& c) {
     if (c.mode == kRender) a.gone_d = 8.0f;
     else if (a.msharp > 0.0f) a.gone_d = std::max(8.0f, 170.0f / (a.msharp * 1.44269504f));
   }
-  if (!a.cull && (c.march->flags & RM_MARCH_TILE16) == 0) a.tiling = 0;
+  if ((c.march->flags & RM_MARCH_ROW_ORDER) != 0) a.tiling = 0;
   if (c.mode == kRender) {  // renderer.rs:27-32, normalised in f32 on the host like the reference
     const float lv[3] = {-0.5f, 0.5f, -1.0f};
     const float len = std::sqrt(lv[0] * lv[0] + lv[1] * lv[1] + lv[2] * lv[2]);

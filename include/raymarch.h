@@ -78,10 +78,10 @@ typedef struct rm_march {
  * off by default because the pre-pass and the uneven block costs lose when few blocks escape.
  * Ignored when t_march or debug outputs are requested. */
 #define RM_MARCH_SKIP_ESCAPED 1
-/* Camera mode: launch 16x16 pixel tiles per 256-ray block (8x8 per wave) instead of rows
- * (implied by RM_MARCH_SKIP_ESCAPED; needs width and height multiples of 16). Changes only the
+/* Camera mode: launch rays in row order instead of 16x16 pixel tiles per 256-ray block (8x8
+ * per wave; the default when width and height are multiples of 16). Changes only the
  * summation order of the gradients. */
-#define RM_MARCH_TILE16 2
+#define RM_MARCH_ROW_ORDER 2
 /* Disable the escaped-ray early exit: by default a wave stops marching once all its rays
  * recede from the scene's bounding sphere at a distance where the silhouette mask is exactly
  * 0 in fp32 (their outputs and gradient terms are then exactly 0, as the full computation

@@ -1,7 +1,7 @@
 """RM_MARCH_SKIP_ESCAPED: skipping ray blocks that provably escape the scene changes nothing.
 
 With the skip on and off (env RM_SKIP_ESCAPED read by native.march_params; both legs in the
-skip's 16x16-tile pixel order, RM_MARCH_TILE16) the forward image,
+default 16x16-tile pixel order) the forward image,
 the train-step loss and every gradient are equal (==; only the sign of an exact zero may
 differ), and the stats counter shows that blocks were actually skipped."""
 import numpy as np
@@ -26,7 +26,6 @@ def _scene(mods, m, seed, radius_range=(0.03, 0.12)):
 
 
 def _both(monkeypatch, fn):
-    monkeypatch.setenv("RM_TILE16", "1")  # the skip's pixel order, so the sums run in the same order
     monkeypatch.setenv("RM_SKIP_ESCAPED", "0")
     full = fn()
     monkeypatch.setenv("RM_SKIP_ESCAPED", "1")
