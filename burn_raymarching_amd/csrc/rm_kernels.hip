@@ -733,7 +733,8 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   float Dprev = INFINITY;  // previous march step (none yet)
   bool dead = false;       // wave-uniform: every ray of the wave has escaped (see below)
   const float c0x = a.centers[0], c0y = a.centers[1], c0z = a.centers[2];
-  const float gone_r = rmax + spread + a.lse_slack;  // bounding sphere around sphere 0, + soft-min slack
+  // R' = bounding sphere around sphere 0 + soft-min slack + 1e-3 (fp32 margin of the march)
+  const float gone_r = rmax + spread + a.lse_slack + 1e-3f;
   if (MODE == kBwd && a.t_in != nullptr) {
     t = a.t_in[ri];
   } else {
@@ -759,10 +760,21 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
         // fp32: out = 0 and every gradient term is 0, whatever the remaining steps would give.
         // A wave whose rays have all escaped stops here. Margins: 1e-5 relative + 1e-3 cover
         // the fp32 rounding of the march at any |p|.
+        // Each remaining step is >= dist - R' long and keeps the ray receding, so the distance
+        // after it is >= sqrt(dist^2 + (dist - R')^2); iterating that bound over the remaining
+        // steps (at most 10 per check) proves the escape long before the ray gets there.
         const float ex = p[0] - c0x, ey = p[1] - c0y, ez = p[2] - c0z;
-        const float dist = sqrtf(fmaf(ez, ez, fmaf(ey, ey, ex * ex)));
-        const bool gone = fmaf(ez, d[2], fmaf(ey, d[1], ex * d[0])) >= 0.0f &&
-                          dist * (1.0f - 1e-5f) - gone_r - 1e-3f >= a.gone_d;
+        bool gone = false;
+        if (fmaf(ez, d[2], fmaf(ey, d[1], ex * d[0])) >= 0.0f) {
+          float dk = sqrtf(fmaf(ez, ez, fmaf(ey, ey, ex * ex))) * (1.0f - 1e-5f);
+          const int nk = min(a.steps - st, 10);
+          for (int k2 = 0; k2 < nk; ++k2) {
+            const float gk = dk - gone_r;
+            if (gk >= a.gone_d || gk <= 0.0f) break;
+            dk = sqrtf(fmaf(gk, gk, dk * dk)) * (1.0f - 1e-5f);
+          }
+          gone = dk - gone_r >= a.gone_d;
+        }
         if (__all(gone || !valid)) {
           dead = true;
           if (a.stats != nullptr && lane == 0) {
@@ -1610,11 +1622,12 @@ int run(rm_context* ctx, const Call& c) {
   a.cull_min_d = c.mode == kRender ? 50.0f : std::max(50.0f, 160.0f / (a.msharp * 1.44269504f));
   a.lse_slack = (float)(std::log((double)M) / (double)a.k * (1.0 + 1e-6)) + 1e-7f;
   // Escaped-ray early exit: the mask must be exactly 0 at distance gone_d -- exp2 of
-  // msharp log2(e) D overflows past 128 (use 170); exp(-10 D^2) underflows long before 8.
+  // msharp log2(e) D overflows at 128 (use 130; the reference's sigmoid(-15 D) is 0 from 5.92);
+  // exp(-10 D^2) underflows long before 6.
   a.gone_d = 0.0f;
   if ((c.march->flags & RM_MARCH_NO_EARLY_EXIT) == 0 && !c.t_out && !c.dbg) {
-    if (c.mode == kRender) a.gone_d = 8.0f;
-    else if (a.msharp > 0.0f) a.gone_d = std::max(8.0f, 170.0f / (a.msharp * 1.44269504f));
+    if (c.mode == kRender) a.gone_d = 6.0f;
+    else if (a.msharp > 0.0f) a.gone_d = std::max(6.0f, 130.0f / (a.msharp * 1.44269504f));
   }
   if ((c.march->flags & RM_MARCH_ROW_ORDER) != 0) a.tiling = 0;
   if (c.mode == kRender) {  // renderer.rs:27-32, normalised in f32 on the host like the reference
