@@ -61,6 +61,8 @@ struct KArgs {
   unsigned long long* stats;  // nullable: [0] += 1 per escaped (skipped) block
   float gone_d;               // > 0: waves whose rays all escaped past this distance stop marching
   const int* esc_flags;       // nullable: per-block escape flags of this launch (rm_escape_kernel)
+  const int* block_order;     // nullable: heavy-first dispatch order of the tiles of a view (ray_block)
+  int order_views, order_tiles;
   CamBasis cams[RM_MAX_VIEWS_PER_CALL];
   // activated scene
   const float* centers;
@@ -537,18 +539,31 @@ __device__ __forceinline__ bool escapes(const float o[3], const float d[3], floa
   return tau >= tc && g(tau) >= (double)min_d;
 }
 
+// Launch position -> logical ray block. With block_order (whole 16x16-tiled views per launch) the
+// blocks are dispatched tile rank by tile rank, the views interleaved, in the order of
+// block_order: the tiles nearest the image centre -- where the scene usually is, and so the
+// rays that march all their steps -- first, the cheap border tiles last, where they fill the
+// machine while the heavy blocks finish. Partials stay indexed by the logical block, so the
+// gradient sums (and every result) do not depend on the order.
+__device__ __forceinline__ long long ray_block(const KArgs& a) {
+  const int b = blockIdx.x;
+  if (a.block_order == nullptr) return b;
+  const int r = b / a.order_views, v = b - r * a.order_views;
+  return (long long)v * a.order_tiles + a.block_order[r];
+}
+
 // A block of escaping rays: out = 0 (requested outputs), zero gradient partials, and for the
 // train step the L1 loss of out = 0, reduced exactly as in the full path.
 template <int MODE>
-__device__ __forceinline__ void escaped_block(const KArgs& a, const Lds& L, long long ri, bool valid, int tid, int lane,
-                                           int wave) {
+__device__ __forceinline__ void escaped_block(const KArgs& a, const Lds& L, long long blk, long long ri, bool valid,
+                                           int tid, int lane, int wave) {
   if (MODE != kBwd && a.out != nullptr && valid) {
     a.out[3 * ri] = 0.0f;
     a.out[3 * ri + 1] = 0.0f;
     a.out[3 * ri + 2] = 0.0f;
   }
   if constexpr (MODE == kFwd || MODE == kRender) return;
-  float* rec = a.partials + (long long)blockIdx.x * a.rec;
+  float* rec = a.partials + blk * a.rec;
   for (long long e = tid; e < (long long)a.Mpad * 12; e += kBlock) rec[e] = 0.0f;
   float loss = 0.0f;
   if (MODE == kTrain && valid) {  // training.rs:17-34 with out = 0
@@ -612,7 +627,8 @@ template <int MODE, bool CAM>
 __global__ __launch_bounds__(kBlock) void rm_escape_kernel(const KArgs a, int* __restrict__ flags) {
   __shared__ float scratch[8 * kWaves];
   const int tid = threadIdx.x;
-  const long long li = (long long)blockIdx.x * kBlock + tid;
+  const long long blk = ray_block(a);
+  const long long li = blk * kBlock + tid;
   const bool valid = li < a.n_rays;
   long long ri = a.ray_begin + (valid ? li : 0);
   float o[3], d[3];
@@ -623,7 +639,7 @@ __global__ __launch_bounds__(kBlock) void rm_escape_kernel(const KArgs a, int* _
   const bool esc = !valid || escapes(o, d, have_t ? a.t_in[ri] : -1.0f, have_t, a.steps, c0, R, a.lse_slack,
                                      a.cull_min_d);
   const int all = __syncthreads_and(esc);
-  if (tid == 0) flags[blockIdx.x] = all;
+  if (tid == 0) flags[blk] = all;
 }
 
 template <int MODE, bool CAM>
@@ -645,7 +661,8 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   L.misc = L.slots + 2 * kWaves * kChunkBwd * 8;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const long long li = (long long)blockIdx.x * kBlock + tid;
+  const long long blk = ray_block(a);
+  const long long li = blk * kBlock + tid;
   const bool valid = li < a.n_rays;
   long long ri = a.ray_begin + (valid ? li : 0);  // becomes the ray's row in the [N,3] tensors
 
@@ -658,9 +675,9 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   // ---- escape skip (RM_MARCH_SKIP_ESCAPED): a block whose rays all provably leave the scene
   // (rm_escape_kernel) gets out = 0 and zero gradients without marching -- exactly what the full
   // computation yields for them, since their silhouette mask is 0 in f32 (see escapes()).
-  if (a.esc_flags != nullptr && a.esc_flags[blockIdx.x]) {
+  if (a.esc_flags != nullptr && a.esc_flags[blk]) {
     if (a.stats != nullptr && tid == 0) atomicAdd(a.stats, 1ull);
-    escaped_block<MODE>(a, L, ri, valid, tid, lane, wave);
+    escaped_block<MODE>(a, L, blk, ri, valid, tid, lane, wave);
     return;
   }
 
@@ -948,7 +965,7 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   const float mg = fmaf(mix[2], gm[2], fmaf(mix[1], gm[1], mix[0] * gm[0]));
   const float b_scale = cmu * frcp(Zb);
 
-  float* rec = a.partials + (long long)blockIdx.x * a.rec;
+  float* rec = a.partials + blk * a.rec;
   float* slots = L.slots;
   int chunk_ctr = 0;
 
@@ -1416,6 +1433,8 @@ struct rm_context {
   void* rec = nullptr;                      // sphere records of the current call (rm_prep_kernel)
   size_t rec_bytes = 0;
   long long stats_blocks = 0;               // ray blocks launched while stats are on
+  int* block_order = nullptr;               // centre-out tile order for order_tx x order_ty tiles
+  int order_tx = 0, order_ty = 0;
 };
 
 namespace {
@@ -1438,6 +1457,29 @@ int fail(rm_context* ctx, int code, const char* fmt, ...) {
     hipError_t e_ = (call);                                                                      \
     if (e_ != hipSuccess) return fail(ctx, RM_ERR_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
   } while (0)
+
+// Centre-out dispatch order of the tx x ty tiles of a view (ray_block): by distance of the
+// tile centre from the image centre, ties by tile index. Built once per image size.
+int ensure_block_order(rm_context* ctx, int tx, int ty) {
+  if (ctx->block_order && ctx->order_tx == tx && ctx->order_ty == ty) return RM_OK;
+  std::vector<int> ord((size_t)tx * ty);
+  for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
+  auto key = [&](int i) {
+    const long long dx = 2LL * (i % tx) + 1 - tx, dy = 2LL * (i / tx) + 1 - ty;
+    return dx * dx + dy * dy;
+  };
+  std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return key(x) < key(y); });
+  if (ctx->block_order) {
+    RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    RM_HIP(ctx, hipFree(ctx->block_order));
+    ctx->block_order = nullptr;
+  }
+  RM_HIP(ctx, hipMalloc(&ctx->block_order, sizeof(int) * ord.size()));
+  RM_HIP(ctx, hipMemcpy(ctx->block_order, ord.data(), sizeof(int) * ord.size(), hipMemcpyHostToDevice));
+  ctx->order_tx = tx;
+  ctx->order_ty = ty;
+  return RM_OK;
+}
 
 int pad_spheres(int M) { return (M + kSphereAlign - 1) / kSphereAlign * kSphereAlign; }
 
@@ -1681,6 +1723,15 @@ int run(rm_context* ctx, const Call& c) {
     a.stats = ctx->stats_dev;
     if (ctx->stats_dev) ctx->stats_blocks += nb;
     a.esc_flags = nullptr;
+    a.block_order = nullptr;
+    const long long npix = (long long)c.W * c.H;
+    if (c.cam && a.tiling == 2 && nb > 1 && done % npix == 0 && nr % npix == 0 && nr == nb * kBlock &&
+        (c.march->flags & RM_MARCH_NATURAL_ORDER) == 0) {
+      if ((rc = ensure_block_order(ctx, c.W / 16, c.H / 16)) != RM_OK) return rc;
+      a.block_order = ctx->block_order;
+      a.order_views = (int)(nr / npix);
+      a.order_tiles = (int)(npix / kBlock);
+    }
     if (nb > 0 && a.cull) {
       if (!ctx->esc_flags) RM_HIP(ctx, hipMalloc(&ctx->esc_flags, sizeof(int) * kMaxBlocksPerLaunch));
       const dim3 g((unsigned)nb);
@@ -1828,10 +1879,11 @@ int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset) {
 
 void rm_destroy(rm_context* ctx) {
   if (!ctx) return;
-  if (ctx->stats_dev || ctx->esc_flags || ctx->rec) {
+  if (ctx->stats_dev || ctx->esc_flags || ctx->rec || ctx->block_order) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stats_dev) (void)hipFree(ctx->stats_dev);
     if (ctx->esc_flags) (void)hipFree(ctx->esc_flags);
+    if (ctx->block_order) (void)hipFree(ctx->block_order);
     if (ctx->rec) (void)hipFree(ctx->rec);
   }
   for (auto& pr : ctx->events) {

@@ -87,6 +87,11 @@ typedef struct rm_march {
  * 0 in fp32 (their outputs and gradient terms are then exactly 0, as the full computation
  * gives). Set for A/B timing; t_march and debug outputs disable it automatically. */
 #define RM_MARCH_NO_EARLY_EXIT 4
+/* Camera mode with 16x16 tiles and whole views per launch: dispatch the ray blocks in launch
+ * order instead of centre-out (tiles nearest the image centre first, views interleaved, so the
+ * blocks that march every step start first and the cheap border blocks fill the tail). The
+ * dispatch order changes no result bit: gradient partials are indexed by tile. A/B timing. */
+#define RM_MARCH_NATURAL_ORDER 8
 
 /* Pinhole LookAt camera, camera.rs:30-37. Rays are generated in-kernel exactly as
  * create_camera_rays (camera.rs:41-87): rows y then x, u = x/W*2-1, v = -(y/H*2-1). */
