@@ -104,9 +104,10 @@ typedef const __attribute__((address_space(4))) f4v* cf4_ptr;
 typedef const __attribute__((address_space(4))) f2v* cf2_ptr;
 typedef const __attribute__((address_space(4))) float* cf1_ptr;
 
-// Header after the records: {r_min, r_max, max |c_j - c_0|, 0} of the real spheres, followed by
-// one partial header per rm_prep_kernel block when that kernel ran on more than one block.
-constexpr int kRecHeader = 4;
+// Header after the records: {r_min, r_max, max |c_j - c_0|, 0, c_x, c_y, c_z, R} of the real
+// spheres ((c, R): bounding sphere, scene_bound), followed by one partial header per
+// rm_prep_kernel block when that kernel ran on more than one block.
+constexpr int kRecHeader = 8;
 
 __host__ __device__ inline size_t rec_bytes(int npairs, int nprep) {
   return (size_t)npairs * (7 * 16 + 8) + (size_t)(nprep + 1) * kRecHeader * sizeof(float);
@@ -163,9 +164,70 @@ __device__ __forceinline__ void header_reduce(float& rmin, float& rmax, float& s
   }
 }
 
+// Bounding sphere of the scene, block-wide: c0 = centre of the centres' bounding box,
+// R >= |c_j - c0| + r_j for every sphere (rounded up). scratch: >= 8*kWaves floats of LDS.
+__device__ __forceinline__ void scene_bound(const KArgs& a, float* scratch, int tid, float c0[3], float& R) {
+  const int lane = tid & 63, wave = tid >> 6;
+  float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  for (int j = tid; j < a.M; j += kBlock)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float c = a.centers[3 * j + k];
+      v[k] = fminf(v[k], c);
+      v[3 + k] = fmaxf(v[3 + k], c);
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      v[k] = fminf(v[k], __shfl_xor(v[k], off));
+      v[3 + k] = fmaxf(v[3 + k], __shfl_xor(v[3 + k], off));
+    }
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < 6; ++k) scratch[8 * wave + k] = v[k];
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    float lo = scratch[k], hi = scratch[3 + k];
+    for (int w = 1; w < kWaves; ++w) {
+      lo = fminf(lo, scratch[8 * w + k]);
+      hi = fmaxf(hi, scratch[8 * w + 3 + k]);
+    }
+    c0[k] = 0.5f * (lo + hi);
+  }
+  float r = 0.0f;
+  for (int j = tid; j < a.M; j += kBlock) {
+    const float dx = a.centers[3 * j] - c0[0], dy = a.centers[3 * j + 1] - c0[1], dz = a.centers[3 * j + 2] - c0[2];
+    r = fmaxf(r, sqrtf(dx * dx + dy * dy + dz * dz) + a.radius[j]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) r = fmaxf(r, __shfl_xor(r, off));
+  __syncthreads();  // everyone has read the box
+  if (lane == 0) scratch[8 * wave] = r;
+  __syncthreads();
+  R = scratch[0];
+  for (int w = 1; w < kWaves; ++w) R = fmaxf(R, scratch[8 * w]);
+  R = R * (1.0f + 1e-5f) + 1e-6f;  // cover the f32 rounding of |c - c0| + r
+  __syncthreads();  // scratch is reused by the caller
+}
+
+// hdr[4..7] = the bounding sphere (c, R) of scene_bound, for the march's escape test.
+__device__ void write_bound(const KArgs& a, float* hdr) {
+  __shared__ float scratch[8 * kWaves];
+  float c[3], R;
+  scene_bound(a, scratch, threadIdx.x, c, R);
+  if (threadIdx.x == 0) {
+    hdr[4] = c[0];
+    hdr[5] = c[1];
+    hdr[6] = c[2];
+    hdr[7] = R;
+  }
+}
+
 // Records of the call (see Lds), one thread per sphere pair. Each block reduces its pairs'
 // {r_min, r_max, spread} into the header (one block) or its partial (several blocks, then
-// rm_prep_finish).
+// rm_prep_finish); the final header also gets the scene's bounding sphere (scene_bound).
 __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a, float4* __restrict__ rec) {
   const int np = a.Mpad / 2;
   float4* P0 = rec;
@@ -225,9 +287,10 @@ __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a, float4* __r
     W[ip] = make_float4(w[0], w[1], wf[0], wf[1]);
   }
   header_reduce(rmin, rmax, spread, gridDim.x == 1 ? hdr : hdr + (size_t)(1 + blockIdx.x) * kRecHeader);
+  if (gridDim.x == 1) write_bound(a, hdr);
 }
 
-__global__ __launch_bounds__(256) void rm_prep_finish(float* __restrict__ hdr, int nprep) {
+__global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, float* __restrict__ hdr, int nprep) {
   float rmin = INFINITY, rmax = 0.0f, spread = 0.0f;
   for (int b = threadIdx.x; b < nprep; b += 256) {
     const float* h = hdr + (size_t)(1 + b) * kRecHeader;
@@ -236,6 +299,7 @@ __global__ __launch_bounds__(256) void rm_prep_finish(float* __restrict__ hdr, i
     spread = fmaxf(spread, h[2]);
   }
   header_reduce(rmin, rmax, spread, hdr);
+  write_bound(a, hdr);
 }
 
 // ---- packed helpers --------------------------------------------------------------------------
@@ -458,55 +522,8 @@ __device__ __forceinline__ void shade_sweep(const float p[3], const Lds& L, int 
   }
 }
 
-// ---- the fused per-ray kernel ----------------------------------------------------------
-// Bounding sphere of the scene, block-wide: c0 = centre of the centres' bounding box,
-// R >= |c_j - c0| + r_j for every sphere (rounded up). scratch: >= 8*kWaves floats of LDS.
-__device__ __forceinline__ void scene_bound(const KArgs& a, float* scratch, int tid, float c0[3], float& R) {
-  const int lane = tid & 63, wave = tid >> 6;
-  float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  for (int j = tid; j < a.M; j += kBlock)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const float c = a.centers[3 * j + k];
-      v[k] = fminf(v[k], c);
-      v[3 + k] = fmaxf(v[3 + k], c);
-    }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      v[k] = fminf(v[k], __shfl_xor(v[k], off));
-      v[3 + k] = fmaxf(v[3 + k], __shfl_xor(v[3 + k], off));
-    }
-  if (lane == 0)
-#pragma unroll
-    for (int k = 0; k < 6; ++k) scratch[8 * wave + k] = v[k];
-  __syncthreads();
-#pragma unroll
-  for (int k = 0; k < 3; ++k) {
-    float lo = scratch[k], hi = scratch[3 + k];
-    for (int w = 1; w < kWaves; ++w) {
-      lo = fminf(lo, scratch[8 * w + k]);
-      hi = fmaxf(hi, scratch[8 * w + 3 + k]);
-    }
-    c0[k] = 0.5f * (lo + hi);
-  }
-  float r = 0.0f;
-  for (int j = tid; j < a.M; j += kBlock) {
-    const float dx = a.centers[3 * j] - c0[0], dy = a.centers[3 * j + 1] - c0[1], dz = a.centers[3 * j + 2] - c0[2];
-    r = fmaxf(r, sqrtf(dx * dx + dy * dy + dz * dz) + a.radius[j]);
-  }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) r = fmaxf(r, __shfl_xor(r, off));
-  __syncthreads();  // everyone has read the box
-  if (lane == 0) scratch[8 * wave] = r;
-  __syncthreads();
-  R = scratch[0];
-  for (int w = 1; w < kWaves; ++w) R = fmaxf(R, scratch[8 * w]);
-  R = R * (1.0f + 1e-5f) + 1e-6f;  // cover the f32 rounding of |c - c0| + r
-  __syncthreads();  // scratch is reused by the caller
-}
 
+// ---- the fused per-ray kernel ----------------------------------------------------------
 // Does the ray provably end (after `steps` march steps, or at the given march t) at scene
 // distance >= min_d, beyond its closest approach to the scene's bounding sphere (c0, R)?
 //  * Every sphere distance is >= |p - c0| - R, and the soft-min is >= the hard min minus
@@ -749,9 +766,10 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   float lb = -INFINITY;  // lower bound on the scene distance at the current point
   float Dprev = INFINITY;  // previous march step (none yet)
   bool dead = false;       // wave-uniform: every ray of the wave has escaped (see below)
-  const float c0x = a.centers[0], c0y = a.centers[1], c0z = a.centers[2];
-  // R' = bounding sphere around sphere 0 + soft-min slack + 1e-3 (fp32 margin of the march)
-  const float gone_r = rmax + spread + a.lse_slack + 1e-3f;
+  // the scene's bounding sphere (c, R) (scene_bound, in the record header); R' = R + soft-min
+  // slack + 1e-3 (fp32 margin of the march)
+  const float c0x = hdr[4], c0y = hdr[5], c0z = hdr[6];
+  const float gone_r = hdr[7] + a.lse_slack + 1e-3f;
   if (MODE == kBwd && a.t_in != nullptr) {
     t = a.t_in[ri];
   } else {
@@ -1696,7 +1714,7 @@ int run(rm_context* ctx, const Call& c) {
     RM_HIP(ctx, hipGetLastError());
     if (nprep > 1) {
       float* hdr = reinterpret_cast<float*>((char*)ctx->rec + (size_t)np * (7 * 16 + 8));
-      hipLaunchKernelGGL(rm_prep_finish, dim3(1), dim3(256), 0, ctx->stream, hdr, nprep);
+      hipLaunchKernelGGL(rm_prep_finish, dim3(1), dim3(256), 0, ctx->stream, a, hdr, nprep);
       RM_HIP(ctx, hipGetLastError());
     }
     a.rec_buf = (const float4*)ctx->rec;
