@@ -23,7 +23,8 @@ Extra objects on the JSON line:
   roofline      -- the dominant kernel (rm_ray_kernel<train>) timed with hipEvents on its own
                    stream inside the timed region; algorithmic FLOP = 16*(S+10)*M per ray
                     counted only for sphere sweeps that actually ran (waves
-                   whose rays all escaped stop early, see early_exit; achieved_all_rays counts
+                   whose rays all escaped stop early, see early_exit, and the normal is one
+                   sweep instead of six; achieved_all_rays counts the full 16*(S+10)*M for
                    every ray); bound "valu" (fp32 vector);
                    traffic = HBM bytes per launch from the committed rocprofv3 PMC summary
                    (profiles/r01_pmc_traffic.json) when present, else null.
@@ -185,9 +186,12 @@ def main():
     # wave that left the march early skips its remaining march steps and the 10 post-march /
     # backward sweeps (its outputs and gradient terms are exactly 0)
     flop_per_ray = FLOP_PER_EVAL * (S + 10) * M
+    # sweeps a wave runs: S march + reconnect + normal + shade + 2 backward = S + 5 (the kernel
+    # takes the normal's six central-difference sweeps as one gradient sweep)
     sweeps_total = waves_total * (S + 10)
-    sweeps_saved = blocks_skipped * 4 * (S + 10) + st["steps_saved"] + st["waves_exited"] * 10
-    executed_frac = max(0.0, 1.0 - sweeps_saved / sweeps_total)
+    waves_post = max(waves_total - blocks_skipped * 4 - st["waves_exited"], 0)
+    sweeps_run = (waves_total - blocks_skipped * 4) * S - st["steps_saved"] + waves_post * 5
+    executed_frac = max(0.0, sweeps_run / sweeps_total)
     flops_launch = flop_per_ray * rays_per_rank * executed_frac
     achieved_tf = flops_launch / (kern_avg_ms * 1e-3) / 1e12
     mpad = (M + 31) // 32 * 32

@@ -470,6 +470,81 @@ __device__ __forceinline__ void lse_taps_w(const float p[3], const Lds& L, int n
   for (int t = 0; t < 6; ++t) s[t] = acc[t].x + acc[t].y;
 }
 
+// Gradient of the soft-min at p for the detached normal: grad D = sum_j beta_j (p - c_j) / rho_j
+// with beta = softmax(-k dist). scene.rs:81-128 takes central differences of D with eps = 1e-4;
+// this is their eps -> 0 limit (they differ by O(eps^2) times the third derivative of D, ~1e-6
+// relative, below the fp32 noise of the reference's own differences). One sweep instead of six:
+// per sphere one rsq and one exp2. e' = k (p - c) in direct form, q' = |e'|^2,
+// rho' = q' rsq(q') = k rho, and the unnormalised weight 2^(k r) 2^(-rho') (SHIFT none),
+// 2^(k(r - r_0)) 2^(rho'_0 - rho') (fixed) or 2^(k r - rho' - m) with a chunked running max m
+// (max): every shift cancels in sum(w u) / sum(w). Returns grad D in g.
+template <bool CLAMP, int SHIFT>
+__device__ __forceinline__ void grad_sweep(const float p[3], const Lds& L, int npairs, float kappa, float (&g)[3]) {
+  const f2 KPX = sp(kappa * p[0]), KPY = sp(kappa * p[1]), KPZ = sp(kappa * p[2]), HK = sp(0.5f * kappa),
+           QMIN = sp(kappa * kappa * 1e-6f);
+  f2 G[3] = {sp(0.0f), sp(0.0f), sp(0.0f)}, Z = sp(0.0f), SH = sp(0.0f);
+  float m = -INFINITY;
+  for (int i0 = 0; i0 < npairs; i0 += 8) {
+    f2 ex[8], ey[8], ez[8], r[8], arg[8];
+#pragma unroll
+    for (int ii = 0; ii < 8; ++ii) {
+      const float4 A = L.p0(i0 + ii), B = L.p1(i0 + ii);
+      ex[ii] = fma2(HK, lo(A), KPX);
+      ey[ii] = fma2(HK, hi(A), KPY);
+      ez[ii] = fma2(HK, lo(B), KPZ);
+      f2 q = fma2(ez[ii], ez[ii], fma2(ey[ii], ey[ii], ex[ii] * ex[ii]));
+      const f2 qraw = q;
+      if constexpr (CLAMP) q = f2{fmaxf(q.x, QMIN.x), fmaxf(q.y, QMIN.y)};
+      r[ii] = f2{frsq(q.x), frsq(q.y)};
+      const f2 rho = q * r[ii];
+      if constexpr (CLAMP) {  // clamp_min(1e-6): that distance is constant, no gradient
+        r[ii].x = qraw.x >= QMIN.x ? r[ii].x : 0.0f;
+        r[ii].y = qraw.y >= QMIN.y ? r[ii].y : 0.0f;
+      }
+      if constexpr (SHIFT == kShiftFixed) {
+        if (i0 == 0 && ii == 0) SH = sp(rho.x);
+        arg[ii] = SH - rho;
+      } else if constexpr (SHIFT == kShiftNone) {
+        arg[ii] = -rho;
+      } else {
+        const float2 K = L.kr(i0 + ii);
+        arg[ii] = f2{K.x, K.y} - rho;
+      }
+    }
+    f2 MN = sp(0.0f);
+    if constexpr (SHIFT == kShiftMax) {
+      float cm = fmaxf(arg[0].x, arg[0].y);
+#pragma unroll
+      for (int ii = 1; ii < 8; ++ii) cm = fmaxf(cm, fmaxf(arg[ii].x, arg[ii].y));
+      const float mn = fmaxf(m, cm);
+      const f2 sc = sp(fexp2(m - mn));
+      Z *= sc;
+      G[0] *= sc;
+      G[1] *= sc;
+      G[2] *= sc;
+      m = mn;
+      MN = sp(mn);
+    }
+#pragma unroll
+    for (int ii = 0; ii < 8; ++ii) {
+      f2 w = exp2v(SHIFT == kShiftMax ? arg[ii] - MN : arg[ii]);
+      if constexpr (SHIFT != kShiftMax) {
+        const f4v Wt = L.W[i0 + ii];
+        w = w * (SHIFT == kShiftFixed ? f2{Wt.z, Wt.w} : f2{Wt.x, Wt.y});
+      }
+      Z += w;
+      const f2 wr = w * r[ii];
+      G[0] = fma2(wr, ex[ii], G[0]);
+      G[1] = fma2(wr, ey[ii], G[1]);
+      G[2] = fma2(wr, ez[ii], G[2]);
+    }
+  }
+  const float iz = frcp(Z.x + Z.y);
+  g[0] = (G[0].x + G[0].y) * iz;
+  g[1] = (G[1].x + G[1].y) * iz;
+  g[2] = (G[2].x + G[2].y) * iz;
+}
+
 // Distances delta_j = rho_j - r_j at p_final for a pair (shade sweep and backward sweep 1 share it).
 template <bool CLAMP>
 __device__ __forceinline__ f2 delta_pair(const f2& PX, const f2& PY, const f2& PZ, const f2& PP, const float4& A,
@@ -852,8 +927,32 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     // p_final is |Da| from p_approx; the taps another eps away
     fast_f = MODE == kRender ? all_safe(lb - a.eps) : all_safe(-mA * inv_kappa - fabsf(Da) - a.eps);
 
-    // ---- detached 6-tap normal (scene.rs:81-128)
-    {
+    // ---- detached normal (scene.rs:81-128): n = f / sqrt(|f|^2 + 1e-6) with f the central
+    // differences (D(p + eps e_a) - D(p - eps e_a))_a; the 1e-6 keeps |n| ~ 0.2 at eps = 1e-4.
+    if constexpr (MODE != kRender) {
+      // f = 2 eps grad D (grad_sweep), shift as in the march at p_final: d_min(p_final) <=
+      // d_min(p_a) + |Da| <= 2 max(Da, 0) + ln(M)/k
+      float gD[3];
+      const int np = a.Mpad / 2;
+      const bool none = shift_none_ok && __all(2.0f * fmaxf(Da, 0.0f) + a.lse_slack <= 90.0f * inv_kappa);
+      const bool fixed = !none && shift_fixed_ok && __all(psq(p) <= 1e10f);
+      if (none) {
+        if (fast_f) grad_sweep<false, kShiftNone>(p, L, np, kappa, gD);
+        else grad_sweep<true, kShiftNone>(p, L, np, kappa, gD);
+      } else if (fixed) {
+        if (fast_f) grad_sweep<false, kShiftFixed>(p, L, np, kappa, gD);
+        else grad_sweep<true, kShiftFixed>(p, L, np, kappa, gD);
+      } else {
+        if (fast_f) grad_sweep<false, kShiftMax>(p, L, np, kappa, gD);
+        else grad_sweep<true, kShiftMax>(p, L, np, kappa, gD);
+      }
+      const float te = 2.0f * a.eps;
+      const float nx = te * gD[0], ny = te * gD[1], nz = te * gD[2];
+      const float inv_len = frsq(fmaf(nz, nz, fmaf(ny, ny, fmaf(nx, nx, 1e-6f))));
+      nrm[0] = nx * inv_len;
+      nrm[1] = ny * inv_len;
+      nrm[2] = nz * inv_len;
+    } else {  // renderer.rs: the six taps themselves
       float m6[6], s6[6];
 #pragma unroll
       for (int q = 0; q < 6; ++q) {
