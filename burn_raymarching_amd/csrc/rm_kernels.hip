@@ -60,6 +60,7 @@ struct KArgs {
   float lse_slack;  // ln(M) / k (rounded up): the hard min exceeds the soft-min by at most this
   unsigned long long* stats;  // nullable: [0] += 1 per escaped (skipped) block
   float gone_d;               // > 0: waves whose rays all escaped past this distance stop marching
+  int mfma;                   // march sums on the matrix cores (lse_mfma) instead of lse_weighted
   const int* esc_flags;       // nullable: per-block escape flags of this launch (rm_escape_kernel)
   const int* block_order;     // nullable: heavy-first dispatch order of the tiles of a view (ray_block)
   int order_views, order_tiles;
@@ -109,14 +110,22 @@ typedef const __attribute__((address_space(4))) float* cf1_ptr;
 // rm_prep_kernel block when that kernel ran on more than one block.
 constexpr int kRecHeader = 8;
 
+// Then, 16-byte aligned, the matrix-core tiles of the march (lse_mfma): per row block of 16
+// spheres 64 lanes x 16 B of A fragments, then per row block 32 floats {w(16), w_fixed(16)}.
+__host__ __device__ inline size_t tiles_offset(int npairs, int nprep) {
+  return ((size_t)npairs * (7 * 16 + 8) + (size_t)(nprep + 1) * kRecHeader * sizeof(float) + 15) & ~(size_t)15;
+}
 __host__ __device__ inline size_t rec_bytes(int npairs, int nprep) {
-  return (size_t)npairs * (7 * 16 + 8) + (size_t)(nprep + 1) * kRecHeader * sizeof(float);
+  const size_t nrb = (size_t)npairs / 8;
+  return tiles_offset(npairs, nprep) + nrb * 64 * 16 + nrb * 32 * sizeof(float);
 }
 
 struct Lds {  // the sphere records (global, scalar-loaded) plus the kernel's LDS scratch
   cf4_ptr P0, P1, P2, P3, S0, S1, W;
   cf2_ptr P4;
-  float* slots;  // backward wave partials, 2 buffers (LDS)
+  const uint4* At;  // lse_mfma sphere fragments (global)
+  const float* Wt;  // lse_mfma weights (global)
+  float* slots;  // backward wave partials, 2 buffers (LDS); lse_mfma's ray exchange in the march
   float* misc;   // small LDS scratch
   __device__ __forceinline__ static float4 v4(f4v v) { return make_float4(v.x, v.y, v.z, v.w); }
   __device__ __forceinline__ float4 p0(int i) const { return v4(P0[i]); }
@@ -133,7 +142,12 @@ struct Lds {  // the sphere records (global, scalar-loaded) plus the kernel's LD
   }
 };
 
-__host__ __device__ constexpr size_t lds_bytes() { return (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float) + 256; }
+// LDS: the backward's two partial buffers, or (during the march) lse_mfma's per-wave ray
+// exchange (64 x (16 + 16 + 4) B per wave); then 256 B of misc scratch.
+constexpr size_t kSlotBytes = (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float) > (size_t)kWaves * 64 * 36
+                                  ? (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float)
+                                  : (size_t)kWaves * 64 * 36;
+__host__ __device__ constexpr size_t lds_bytes() { return kSlotBytes + 256; }
 
 // three-value block reduction (min, max, max) for the record header
 __device__ __forceinline__ void header_reduce(float& rmin, float& rmax, float& spread, float* dst) {
@@ -212,6 +226,48 @@ __device__ __forceinline__ void scene_bound(const KArgs& a, float* scratch, int 
   __syncthreads();  // scratch is reused by the caller
 }
 
+// ---- matrix-core march fragments (see lse_mfma) ----------------------------------------------
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// exact three-part bf16 split of x (bit patterns in the low 16 bits)
+__device__ __forceinline__ void split3(float x, unsigned& h1, unsigned& h2, unsigned& h3) {
+  const unsigned a = __float_as_uint(x) & 0xFFFF0000u;
+  const float r1 = x - __uint_as_float(a);
+  const unsigned b = __float_as_uint(r1) & 0xFFFF0000u;
+  const float r2 = r1 - __uint_as_float(b);
+  const unsigned c = __float_as_uint(r2) & 0xFFFF0000u;
+  h1 = a >> 16;
+  h2 = b >> 16;
+  h3 = c >> 16;
+}
+__device__ __forceinline__ unsigned pack2(unsigned lo16, unsigned hi16) { return lo16 | (hi16 << 16); }
+constexpr unsigned kBf16One = 0x3F80u;
+
+// sphere-side fragment of lane l for row block rb (rm_prep_kernel)
+__device__ __forceinline__ uint4 mfma_a_frag(const KArgs& a, int rb, int l) {
+  const int j = 16 * rb + (l & 15), g = l >> 4;
+  const float kappa = a.k * kLog2e, k2 = kappa * kappa;
+  float cx, cy, cz;
+  if (j < a.M) {
+    cx = a.centers[3 * j];
+    cy = a.centers[3 * j + 1];
+    cz = a.centers[3 * j + 2];
+  } else {  // padding sphere (see rm_prep_kernel)
+    cx = kPadCenter;
+    cy = cz = 0.0f;
+  }
+  unsigned x[3], y[3], z[3], C[3];
+  split3(-2.0f * k2 * cx, x[0], x[1], x[2]);
+  split3(-2.0f * k2 * cy, y[0], y[1], y[2]);
+  split3(-2.0f * k2 * cz, z[0], z[1], z[2]);
+  split3(k2 * (cx * cx + cy * cy + cz * cz), C[0], C[1], C[2]);
+  if (g < 2)
+    return make_uint4(pack2(x[g], x[g]), pack2(x[g], y[g]), pack2(y[g], y[g]), pack2(z[g], z[g]));
+  if (g == 2) return make_uint4(pack2(x[2], x[2]), pack2(0u, y[2]), pack2(y[2], 0u), pack2(z[2], z[2]));
+  return make_uint4(pack2(z[0], z[1]), pack2(kBf16One, kBf16One), pack2(kBf16One, C[0]), pack2(C[1], C[2]));
+}
+
 // hdr[4..7] = the bounding sphere (c, R) of scene_bound, for the march's escape test.
 __device__ void write_bound(const KArgs& a, float* hdr) {
   __shared__ float scratch[8 * kWaves];
@@ -285,6 +341,17 @@ __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a, float4* __r
     S0[ip] = make_float4(k2 * gx[0], k2 * gx[1], k2 * gy[0], k2 * gy[1]);
     S1[ip] = make_float4(k2 * gz[0], k2 * gz[1], k2 * cc[0], k2 * cc[1]);
     W[ip] = make_float4(w[0], w[1], wf[0], wf[1]);
+  }
+  // matrix-core tiles of the march (lse_mfma)
+  const int nrb = np / 8;
+  char* tiles = reinterpret_cast<char*>(rec) + tiles_offset(np, gridDim.x);
+  uint4* At = reinterpret_cast<uint4*>(tiles);
+  float* Wt = reinterpret_cast<float*>(At + (size_t)nrb * 64);
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < nrb * 64; e += gridDim.x * 256) At[e] = mfma_a_frag(a, e >> 6, e & 63);
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < nrb * 32; e += gridDim.x * 256) {
+    const int j = 16 * (e >> 5) + (e & 15);
+    const float krj = j < a.M ? kappa * a.radius[j] : 0.0f;
+    Wt[e] = j >= a.M ? 0.0f : ((e & 16) ? fexp2(krj - kr_first) : fexp2(krj));
   }
   header_reduce(rmin, rmax, spread, gridDim.x == 1 ? hdr : hdr + (size_t)(1 + blockIdx.x) * kRecHeader);
   if (gridDim.x == 1) write_bound(a, hdr);
@@ -367,6 +434,82 @@ __device__ __forceinline__ void lse_point(const float p[3], const Lds& L, int np
     s = acc.x + acc.y;
     m = mn;
   }
+}
+
+// ---- the march's log-sum-exp on the matrix cores ---------------------------------------------
+// q'_jn = k^2 |p_n - c_j|^2 for 16 spheres x 16 rays is one v_mfma_f32_16x16x32_bf16: every f32
+// operand is split exactly into three bf16 parts (x = x1 + x2 + x3, truncation: each part keeps
+// the next 8 significant bits), and the K = 32 products are the 30 split-part products that
+// matter (a3 x3 is below 2^-30 of a x), all exact in fp32:
+//   K slice 0: A = [a1x a1x a1x a1y a1y a1y a1z a1z]   B = Sa = [x1 x2 x3 y1 y2 y3 z1 z2]
+//   K slice 1: A = [a2x a2x a2x a2y a2y a2y a2z a2z]   B = Sa
+//   K slice 2: A = [a3x a3x 0   a3y a3y 0   a3z a3z]   B = Sa
+//   K slice 3: A = [a1z a2z 1 1 1 C1 C2 C3]             B = Sb = [z3 z3 P1 P2 P3 1 1 1]
+// with a = -2 k^2 c, C = k^2 |c|^2 (sphere side, rm_prep_kernel) and P = k^2 |p|^2 (ray side):
+// sum = k^2 (|p|^2 - 2 p.c + |c|^2), the expansion form of scene.rs:66-71. The lanes then run
+// only sqrt, exp2 and the weighted accumulate (lse_weighted's four packed ops per sphere pair
+// go to the matrix pipe). Lane (n, g) = (l & 15, l >> 4) holds rays 16cb + n of the wave and
+// spheres 16rb + 4g + v; the rays' Sa / Sb / shift go through a per-wave LDS exchange.
+// Sum over the spheres of w_j 2^(-rho'_j) (FIXED = false; w = 2^(k r)) or w_j 2^(sh - rho'_j)
+// (FIXED; w = 2^(k (r - r_0)), sh = the ray's own shift) for the lane's own ray -- the same sum
+// as lse_weighted up to fp32 rounding. xa / xb / xs: this wave's LDS exchange (64 uint4, 64
+// uint4, 64 floats).
+template <bool CLAMP, bool FIXED>
+__device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, const uint4* __restrict__ At,
+                                          const float* __restrict__ Wt, int nrb, uint4* xa, uint4* xb, float* xs,
+                                          int lane) {
+  {  // the lane's own ray: Sa, Sb and the shift into the exchange
+    unsigned x[3], y[3], z[3], P[3];
+    split3(p[0], x[0], x[1], x[2]);
+    split3(p[1], y[0], y[1], y[2]);
+    split3(p[2], z[0], z[1], z[2]);
+    split3(k2 * psq(p), P[0], P[1], P[2]);
+    xa[lane] = make_uint4(pack2(x[0], x[1]), pack2(x[2], y[0]), pack2(y[1], y[2]), pack2(z[0], z[1]));
+    xb[lane] = make_uint4(pack2(z[2], z[2]), pack2(P[0], P[1]), pack2(P[2], kBf16One), pack2(kBf16One, kBf16One));
+    if constexpr (FIXED) xs[lane] = sh;
+  }
+  __builtin_amdgcn_wave_barrier();
+  const int n = lane & 15, g = lane >> 4;
+  const uint4* src = g < 3 ? xa : xb;
+  bf16x8 B[4];
+  float S[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    B[cb] = __builtin_bit_cast(bf16x8, src[16 * cb + n]);
+    S[cb] = FIXED ? xs[16 * cb + n] : 0.0f;
+  }
+  const float QMIN = k2 * 1e-6f;
+  float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  const f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int rb = 0; rb < nrb; ++rb) {
+    const bf16x8 A = __builtin_bit_cast(bf16x8, At[rb * 64 + lane]);
+    const float4 w = *reinterpret_cast<const float4*>(Wt + rb * 32 + (FIXED ? 16 : 0) + 4 * g);
+    f32x4 D[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) D[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[cb], zero, 0, 0, 0);
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      float q[4] = {D[cb].x, D[cb].y, D[cb].z, D[cb].w};
+      const float wv[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        if constexpr (CLAMP) q[v] = fmaxf(q[v], QMIN);
+        const float rho = fsqrt(q[v]);
+        acc[cb] = fmaf(wv[v], fexp2(FIXED ? S[cb] - rho : -rho), acc[cb]);
+      }
+    }
+  }
+  // partial sums of ray 16cb + n sit in the four lane groups: reduce across them, keep own ray
+  float own = 0.0f;
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    float s = acc[cb];
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    if (cb == g) own = s;
+  }
+  __builtin_amdgcn_wave_barrier();  // the exchange is rewritten by the next step
+  return own;
 }
 
 // The march's log-sum-exp in weighted form: rho' = sqrt(k^2 q) = k rho straight from the scaled
@@ -748,9 +891,11 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     L.S1 = L.S0 + np;
     L.W = L.S1 + np;
     L.P4 = (cf2_ptr)(L.W + np);
+    L.At = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(a.rec_buf) + tiles_offset(np, (np + 255) / 256));
+    L.Wt = reinterpret_cast<const float*>(L.At + (size_t)(np / 8) * 64);
   }
   L.slots = reinterpret_cast<float*>(smem);
-  L.misc = L.slots + 2 * kWaves * kChunkBwd * 8;
+  L.misc = L.slots + kSlotBytes / sizeof(float);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long long blk = ray_block(a);
@@ -807,6 +952,27 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     const bool none = shift_none_ok && __all(2.0f * fmaxf(Dprev, 0.0f) + a.lse_slack <= 90.0f * inv_kappa);
     float m = none ? 0.0f : -INFINITY, s = 0.0f;
     const bool fixed = !none && shift_fixed_ok && __all(psq(p) <= 1e10f);
+    if ((none || fixed) && a.mfma) {
+      const float k2 = kappa * kappa;
+      float sh = 0.0f;
+      if (fixed) {  // the ray's shift: rho'_0 of sphere 0 (any value near it keeps +-100 headroom)
+        const float4 A = Lds::v4(L.S0[0]), B = Lds::v4(L.S1[0]);
+        float q0 = fmaf(p[2], B.x, fmaf(p[1], A.z, fmaf(p[0], A.x, fmaf(k2, psq(p), B.z))));
+        sh = fsqrt(fmaxf(q0, k2 * 1e-6f));
+      }
+      const int nrb = a.Mpad / 16;
+      uint4* xa = reinterpret_cast<uint4*>(L.slots) + wave * 64;
+      uint4* xb = reinterpret_cast<uint4*>(L.slots) + kWaves * 64 + wave * 64;
+      float* xs = L.slots + kWaves * 64 * 8 + wave * 64;
+      if (none)
+        s = fast ? lse_mfma<false, false>(p, k2, sh, L.At, L.Wt, nrb, xa, xb, xs, lane)
+                 : lse_mfma<true, false>(p, k2, sh, L.At, L.Wt, nrb, xa, xb, xs, lane);
+      else
+        s = fast ? lse_mfma<false, true>(p, k2, sh, L.At, L.Wt, nrb, xa, xb, xs, lane)
+                 : lse_mfma<true, true>(p, k2, sh, L.At, L.Wt, nrb, xa, xb, xs, lane);
+      if (fixed) m = kr_first - sh;
+      return -(flog2(fmaxf(s, 1e-30f)) + m) * inv_kappa;
+    }
     if (none || fixed) {
       const float k2 = kappa * kappa;
       const int np = a.Mpad / 2;
@@ -1789,6 +1955,7 @@ int run(rm_context* ctx, const Call& c) {
     else if (a.msharp > 0.0f) a.gone_d = std::max(6.0f, 130.0f / (a.msharp * 1.44269504f));
   }
   if ((c.march->flags & RM_MARCH_ROW_ORDER) != 0) a.tiling = 0;
+  a.mfma = (c.march->flags & RM_MARCH_VALU_ONLY) == 0;
   if (c.mode == kRender) {  // renderer.rs:27-32, normalised in f32 on the host like the reference
     const float lv[3] = {-0.5f, 0.5f, -1.0f};
     const float len = std::sqrt(lv[0] * lv[0] + lv[1] * lv[1] + lv[2] * lv[2]);

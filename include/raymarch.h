@@ -92,6 +92,11 @@ typedef struct rm_march {
  * blocks that march every step start first and the cheap border blocks fill the tail). The
  * dispatch order changes no result bit: gradient partials are indexed by tile. A/B timing. */
 #define RM_MARCH_NATURAL_ORDER 8
+/* Run the march's sphere sums on the vector units only. By default the squared distances of
+ * the unshifted / fixed-shift march steps come from bf16 matrix-core products of exact
+ * three-part splits of the fp32 operands (equal to the fp32 expansion form to rounding) and
+ * the vector units do only sqrt, exp2 and the accumulate. A/B timing. */
+#define RM_MARCH_VALU_ONLY 16
 
 /* Pinhole LookAt camera, camera.rs:30-37. Rays are generated in-kernel exactly as
  * create_camera_rays (camera.rs:41-87): rows y then x, u = x/W*2-1, v = -(y/H*2-1). */
