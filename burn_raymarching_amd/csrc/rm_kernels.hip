@@ -481,12 +481,14 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
   const float QMIN = k2 * 1e-6f;
   float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   const f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (int rb = 0; rb < nrb; ++rb) {
-    const bf16x8 A = __builtin_bit_cast(bf16x8, At[rb * 64 + lane]);
-    const float4 w = *reinterpret_cast<const float4*>(Wt + rb * 32 + (FIXED ? 16 : 0) + 4 * g);
-    f32x4 D[4];
+  const float* wsrc = Wt + (FIXED ? 16 : 0) + 4 * g;
+  auto load_a = [&](int rb) { return __builtin_bit_cast(bf16x8, At[rb * 64 + lane]); };
+  auto load_w = [&](int rb) { return *reinterpret_cast<const float4*>(wsrc + rb * 32); };
+  auto tile = [&](const bf16x8& A, f32x4 (&D)[4]) {
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) D[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[cb], zero, 0, 0, 0);
+  };
+  auto consume = [&](const f32x4 (&D)[4], const float4& w) {
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       float q[4] = {D[cb].x, D[cb].y, D[cb].z, D[cb].w};
@@ -498,6 +500,28 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
         acc[cb] = fmaf(wv[v], fexp2(FIXED ? S[cb] - rho : -rho), acc[cb]);
       }
     }
+  };
+  // two tiles in flight: the matrix pipe computes row block rb + 1 while the lanes finish rb,
+  // and the fragments are loaded one tile ahead (nrb is even: Mpad % 32 == 0; the last
+  // iteration recomputes block nrb - 1 into a tile it never reads)
+  f32x4 D0[4], D1[4];
+  bf16x8 A1 = load_a(1);
+  tile(load_a(0), D0);
+  float4 w0 = load_w(0);
+  for (int rb = 0; rb < nrb; rb += 2) {
+    tile(A1, D1);
+    const float4 w1 = load_w(rb + 1);
+    const int r2 = min(rb + 2, nrb - 1), r3 = min(rb + 3, nrb - 1);
+    const bf16x8 A0 = load_a(r2);
+    __builtin_amdgcn_sched_barrier(0);  // keep the loads a tile ahead of their use
+    consume(D0, w0);
+    __builtin_amdgcn_sched_barrier(0);
+    tile(A0, D0);
+    w0 = load_w(r2);
+    A1 = load_a(r3);
+    __builtin_amdgcn_sched_barrier(0);
+    consume(D1, w1);
+    __builtin_amdgcn_sched_barrier(0);
   }
   // partial sums of ray 16cb + n sit in the four lane groups: reduce across them, keep own ray
   float own = 0.0f;
