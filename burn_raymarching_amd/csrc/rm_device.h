@@ -15,7 +15,10 @@ namespace rm {
 #define RM_BLOCK 256
 #endif
 constexpr int kBlock = RM_BLOCK;         // threads per block (256 = 4 waves)
-constexpr int kMinWavesPerSimd = 4;      // register budget: <= 128 VGPRs
+#ifndef RM_MIN_WAVES
+#define RM_MIN_WAVES 4
+#endif
+constexpr int kMinWavesPerSimd = RM_MIN_WAVES;  // register budget: 4 -> <= 128 VGPRs
 constexpr int kWaves = kBlock / 64;
 constexpr int kSphereAlign = 32;         // M is padded to a multiple of this
 constexpr int kChunkBwd = 32;            // spheres per backward partial-combine chunk

@@ -501,26 +501,24 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
       }
     }
   };
-  // two tiles in flight: the matrix pipe computes row block rb + 1 while the lanes finish rb,
-  // and the fragments are loaded one tile ahead (nrb is even: Mpad % 32 == 0; the last
-  // iteration recomputes block nrb - 1 into a tile it never reads)
-  f32x4 D0[4], D1[4];
-  bf16x8 A1 = load_a(1);
-  tile(load_a(0), D0);
-  float4 w0 = load_w(0);
+  // one tile at a time (registers: the march must not spill at 128 VGPRs); the fragments of the
+  // next row block load while the lanes work on this one (nrb is even: Mpad % 32 == 0)
+  f32x4 D[4];
+  bf16x8 A = load_a(0);
+  float4 w = load_w(0);
   for (int rb = 0; rb < nrb; rb += 2) {
-    tile(A1, D1);
+    tile(A, D);
+    const bf16x8 A1 = load_a(rb + 1);
     const float4 w1 = load_w(rb + 1);
-    const int r2 = min(rb + 2, nrb - 1), r3 = min(rb + 3, nrb - 1);
-    const bf16x8 A0 = load_a(r2);
     __builtin_amdgcn_sched_barrier(0);  // keep the loads a tile ahead of their use
-    consume(D0, w0);
+    consume(D, w);
     __builtin_amdgcn_sched_barrier(0);
-    tile(A0, D0);
-    w0 = load_w(r2);
-    A1 = load_a(r3);
+    tile(A1, D);
+    const int rn = min(rb + 2, nrb - 1);
+    A = load_a(rn);
+    w = load_w(rn);
     __builtin_amdgcn_sched_barrier(0);
-    consume(D1, w1);
+    consume(D, w1);
     __builtin_amdgcn_sched_barrier(0);
   }
   // partial sums of ray 16cb + n sit in the four lane groups: reduce across them, keep own ray
