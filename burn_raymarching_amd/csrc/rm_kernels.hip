@@ -115,9 +115,14 @@ constexpr int kRecHeader = 8;
 __host__ __device__ inline size_t tiles_offset(int npairs, int nprep) {
   return ((size_t)npairs * (7 * 16 + 8) + (size_t)(nprep + 1) * kRecHeader * sizeof(float) + 15) & ~(size_t)15;
 }
-__host__ __device__ inline size_t rec_bytes(int npairs, int nprep) {
+// Then the escape thresholds of the march: kEscTab floats (see write_bound).
+constexpr int kEscTab = 64;
+__host__ __device__ inline size_t esc_offset(int npairs, int nprep) {
   const size_t nrb = (size_t)npairs / 8;
   return tiles_offset(npairs, nprep) + nrb * 64 * 16 + nrb * 32 * sizeof(float);
+}
+__host__ __device__ inline size_t rec_bytes(int npairs, int nprep) {
+  return esc_offset(npairs, nprep) + kEscTab * sizeof(float);
 }
 
 struct Lds {  // the sphere records (global, scalar-loaded) plus the kernel's LDS scratch
@@ -268,8 +273,15 @@ __device__ __forceinline__ uint4 mfma_a_frag(const KArgs& a, int rb, int l) {
   return make_uint4(pack2(z[0], z[1]), pack2(kBf16One, kBf16One), pack2(kBf16One, C[0]), pack2(C[1], C[2]));
 }
 
-// hdr[4..7] = the bounding sphere (c, R) of scene_bound, for the march's escape test.
-__device__ void write_bound(const KArgs& a, float* hdr) {
+// hdr[4..7] = the bounding sphere (c, R) of scene_bound, for the march's escape test, and its
+// distance thresholds T(n), n < kEscTab: a receding ray at distance d from c with n march steps
+// left ends them at distance >= gone_d + R' from c if (1 - 1e-5) d >= T(n). Every step is at
+// least g = d - R' long (R' = R + ln(M)/k + 1e-3: the soft-min is >= the hard min - ln(M)/k,
+// 1e-3 covers the fp32 march) and keeps the ray receding, so one step takes d to at least
+// F(d) = (1 - 1e-5) sqrt(d^2 + (d - R')^2); T(0) = gone_d + R' and T(n) = F^-1(T(n - 1)) =
+// (R' + sqrt(2 y^2 - R'^2)) / 2 with y = T(n - 1) / (1 - 1e-5), rounded up. For n >= kEscTab the
+// march uses T(kEscTab - 1) >= T(n).
+__device__ void write_bound(const KArgs& a, float* hdr, float* esc) {
   __shared__ float scratch[8 * kWaves];
   float c[3], R;
   scene_bound(a, scratch, threadIdx.x, c, R);
@@ -278,6 +290,19 @@ __device__ void write_bound(const KArgs& a, float* hdr) {
     hdr[5] = c[1];
     hdr[6] = c[2];
     hdr[7] = R;
+  }
+  if (threadIdx.x < kEscTab) {
+    float tv = INFINITY;
+    if (a.gone_d > 0.0f) {
+      const double rp = (double)R + (double)a.lse_slack + 1e-3;
+      double T = (double)a.gone_d + rp;
+      for (int n = 1; n <= (int)threadIdx.x; ++n) {
+        const double y = T / (1.0 - 1e-5);
+        T = 0.5 * (rp + sqrt(2.0 * y * y - rp * rp)) * (1.0 + 1e-6) + 1e-6;
+      }
+      tv = (float)(T * (1.0 + 1e-6));
+    }
+    esc[threadIdx.x] = tv;
   }
 }
 
@@ -354,10 +379,11 @@ __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a, float4* __r
     Wt[e] = j >= a.M ? 0.0f : ((e & 16) ? fexp2(krj - kr_first) : fexp2(krj));
   }
   header_reduce(rmin, rmax, spread, gridDim.x == 1 ? hdr : hdr + (size_t)(1 + blockIdx.x) * kRecHeader);
-  if (gridDim.x == 1) write_bound(a, hdr);
+  if (gridDim.x == 1) write_bound(a, hdr, reinterpret_cast<float*>(reinterpret_cast<char*>(rec) + esc_offset(np, 1)));
 }
 
-__global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, float* __restrict__ hdr, int nprep) {
+__global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, float* __restrict__ hdr, float* __restrict__ esc,
+                                                      int nprep) {
   float rmin = INFINITY, rmax = 0.0f, spread = 0.0f;
   for (int b = threadIdx.x; b < nprep; b += 256) {
     const float* h = hdr + (size_t)(1 + b) * kRecHeader;
@@ -366,7 +392,7 @@ __global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, float* __re
     spread = fmaxf(spread, h[2]);
   }
   header_reduce(rmin, rmax, spread, hdr);
-  write_bound(a, hdr);
+  write_bound(a, hdr, esc);
 }
 
 // ---- packed helpers --------------------------------------------------------------------------
@@ -1032,7 +1058,7 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   // the scene's bounding sphere (c, R) (scene_bound, in the record header); R' = R + soft-min
   // slack + 1e-3 (fp32 margin of the march)
   const float c0x = hdr[4], c0y = hdr[5], c0z = hdr[6];
-  const float gone_r = hdr[7] + a.lse_slack + 1e-3f;
+  const cf1_ptr esc_tab = (cf1_ptr)(reinterpret_cast<const char*>(a.rec_buf) + esc_offset(a.Mpad / 2, (a.Mpad / 2 + 255) / 256));
   if (MODE == kBwd && a.t_in != nullptr) {
     t = a.t_in[ri];
   } else {
@@ -1059,20 +1085,12 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
         // A wave whose rays have all escaped stops here. Margins: 1e-5 relative + 1e-3 cover
         // the fp32 rounding of the march at any |p|.
         // Each remaining step is >= dist - R' long and keeps the ray receding, so the distance
-        // after it is >= sqrt(dist^2 + (dist - R')^2); iterating that bound over the remaining
-        // steps (at most 10 per check) proves the escape long before the ray gets there.
+        // grows step by step (write_bound): with n steps left the ray is gone once
+        // (1 - 1e-5) dist >= T(n) -- proven long before the ray gets there.
         const float ex = p[0] - c0x, ey = p[1] - c0y, ez = p[2] - c0z;
-        bool gone = false;
-        if (fmaf(ez, d[2], fmaf(ey, d[1], ex * d[0])) >= 0.0f) {
-          float dk = sqrtf(fmaf(ez, ez, fmaf(ey, ey, ex * ex))) * (1.0f - 1e-5f);
-          const int nk = min(a.steps - st, 10);
-          for (int k2 = 0; k2 < nk; ++k2) {
-            const float gk = dk - gone_r;
-            if (gk >= a.gone_d || gk <= 0.0f) break;
-            dk = sqrtf(fmaf(gk, gk, dk * dk)) * (1.0f - 1e-5f);
-          }
-          gone = dk - gone_r >= a.gone_d;
-        }
+        const float Tn = esc_tab[min(a.steps - st, kEscTab - 1)];
+        const bool gone = fmaf(ez, d[2], fmaf(ey, d[1], ex * d[0])) >= 0.0f &&
+                          fsqrt(fmaf(ez, ez, fmaf(ey, ey, ex * ex))) * (1.0f - 1e-5f) >= Tn;
         if (__all(gone || !valid)) {
           dead = true;
           if (a.stats != nullptr && lane == 0) {
@@ -2002,7 +2020,8 @@ int run(rm_context* ctx, const Call& c) {
     RM_HIP(ctx, hipGetLastError());
     if (nprep > 1) {
       float* hdr = reinterpret_cast<float*>((char*)ctx->rec + (size_t)np * (7 * 16 + 8));
-      hipLaunchKernelGGL(rm_prep_finish, dim3(1), dim3(256), 0, ctx->stream, a, hdr, nprep);
+      float* esc = reinterpret_cast<float*>((char*)ctx->rec + esc_offset(np, nprep));
+      hipLaunchKernelGGL(rm_prep_finish, dim3(1), dim3(256), 0, ctx->stream, a, hdr, esc, nprep);
       RM_HIP(ctx, hipGetLastError());
     }
     a.rec_buf = (const float4*)ctx->rec;

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Build libraymarch_hip.so from a git revision of the kernel source into lib/var/<name>.so, for
+# same-box A/B timing (RM_LIB_PATH=burn_raymarching_amd/lib/var/<name>.so).
+#   bash tools/build_variant.sh <rev> <name> [extra hipcc flags]
+set -e
+REV=$1; NAME=$2; shift 2
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+CS=$ROOT/burn_raymarching_amd/csrc
+mkdir -p "$ROOT/burn_raymarching_amd/lib/var"
+git -C "$ROOT" show "$REV:burn_raymarching_amd/csrc/rm_kernels.hip" > "$CS/_variant.hip"
+git -C "$ROOT" show "$REV:burn_raymarching_amd/csrc/rm_device.h" > "$CS/_variant_device.h"
+sed -i 's/#include "rm_device.h"/#include "_variant_device.h"/' "$CS/_variant.hip"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared -Wno-unused-result "$@" \
+  -o "$ROOT/burn_raymarching_amd/lib/var/$NAME.so" "$CS/_variant.hip"
+rm -f "$CS/_variant.hip" "$CS/_variant_device.h"
+echo "built lib/var/$NAME.so from $REV"
