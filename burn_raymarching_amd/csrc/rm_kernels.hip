@@ -4,21 +4,25 @@
 // Hot path replaced: render_diff (renderer_diff.rs:6-91) and its burn-autodiff
 // backward (train.rs:189-190). One thread owns one ray for the whole pipeline:
 //
-//   in-kernel camera ray (camera.rs:58-78)
+//   in-kernel camera ray (camera.rs:58-78), 16x16 pixel tiles per block, centre-out dispatch
 //   S fixed soft-min march steps          (renderer_diff.rs:20-26, scene.rs:60-79, sdf.rs:30-44)
+//     squared distances on the matrix cores (bf16 three-way splits, lse_mfma), sqrt/exp2 on
+//     the vector units; waves whose rays provably escape leave early (exact)
 //   gradient reconnect sweep at p_approx  (renderer_diff.rs:28-39)
-//   6-tap finite-difference normal        (renderer_diff.rs:41-46, scene.rs:81-128)
+//   detached normal: one soft-min gradient sweep, the eps -> 0 limit of the six central
+//     differences of scene.rs:81-128 (renderer.rs mode: the six taps)
 //   Lambert + ambient                     (renderer_diff.rs:48-62)
 //   softmax colour blend + mask soft-min  (renderer_diff.rs:64-90), one shared sweep
 //   [train] weighted-L1 seed              (training.rs:17-34)
 //   [bwd]   analytic backward: sweep at p_final, then at p_approx
 //
-// Spheres are staged once per workgroup in LDS (float4 {-2c, |c|^2}, float2 {k*log2e*r, r},
-// float4 colour) and read as wave-uniform broadcasts. The soft-min log-sum-exp runs in
-// base 2 on v_exp_f32/v_log_f32 with a chunked running max (one rescale per 8-16 spheres,
-// one exp per sphere). Per-sphere gradients are summed over the 64 rays of a wave with a
-// transposing permlane/DPP reduction, over the 4 waves in LDS, and over workgroups in a
-// fixed order by rm_reduce_partials + rm_finalize_grads (deterministic; no atomics).
+// Sphere records are built once per call (rm_prep_kernel) and read through the constant
+// address space into SGPRs (vector sweeps, two spheres per packed instruction) or as bf16
+// MFMA fragments (march). The soft-min log-sum-exp runs in base 2 on v_exp_f32/v_log_f32 with
+// the cheapest provably safe shift. Per-sphere gradients are summed over the 64 rays of a
+// wave with a transposing permlane/DPP reduction, over the live waves in LDS, and over
+// workgroups in a fixed order by rm_reduce_partials + rm_finalize_grads (deterministic; no
+// atomics). DESIGN.md §4 has the details and the measurements.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
