@@ -24,6 +24,7 @@
 // workgroups in a fixed order by rm_reduce_partials + rm_finalize_grads (deterministic; no
 // atomics). DESIGN.md §4 has the details and the measurements.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cstdarg>
@@ -1921,11 +1922,13 @@ void launch_escape(bool cam, dim3 grid, hipStream_t st, const KArgs& a, int* fla
 }
 
 template <int MODE>
-void launch_ray(bool cam, dim3 grid, size_t lds, hipStream_t st, const KArgs& a) {
+void launch_ray(bool cam, dim3 grid, size_t lds, hipStream_t st, const KArgs& a, hipEvent_t ev0, hipEvent_t ev1) {
+  // With timing on, the start/stop timestamps come from the kernel's own dispatch packet
+  // (hipExtLaunchKernel): no extra barrier packets or cache flushes around the launch.
   if (cam)
-    hipLaunchKernelGGL((rm_ray_kernel<MODE, true>), grid, dim3(kBlock), lds, st, a);
+    hipExtLaunchKernelGGL((rm_ray_kernel<MODE, true>), grid, dim3(kBlock), (uint32_t)lds, st, ev0, ev1, 0u, a);
   else
-    hipLaunchKernelGGL((rm_ray_kernel<MODE, false>), grid, dim3(kBlock), lds, st, a);
+    hipExtLaunchKernelGGL((rm_ray_kernel<MODE, false>), grid, dim3(kBlock), (uint32_t)lds, st, ev0, ev1, 0u, a);
 }
 
 int run(rm_context* ctx, const Call& c) {
@@ -2083,15 +2086,13 @@ int run(rm_context* ctx, const Call& c) {
         ev0 = ctx->events[ctx->events_used].first;
         ev1 = ctx->events[ctx->events_used].second;
         ++ctx->events_used;
-        RM_HIP(ctx, hipEventRecord(ev0, ctx->stream));
       }
       dim3 grid((unsigned)nb);
-      if (c.mode == kFwd) launch_ray<kFwd>(c.cam, grid, lds, ctx->stream, a);
-      else if (c.mode == kBwd) launch_ray<kBwd>(c.cam, grid, lds, ctx->stream, a);
-      else if (c.mode == kTrain) launch_ray<kTrain>(c.cam, grid, lds, ctx->stream, a);
-      else launch_ray<kRender>(c.cam, grid, lds, ctx->stream, a);
+      if (c.mode == kFwd) launch_ray<kFwd>(c.cam, grid, lds, ctx->stream, a, ev0, ev1);
+      else if (c.mode == kBwd) launch_ray<kBwd>(c.cam, grid, lds, ctx->stream, a, ev0, ev1);
+      else if (c.mode == kTrain) launch_ray<kTrain>(c.cam, grid, lds, ctx->stream, a, ev0, ev1);
+      else launch_ray<kRender>(c.cam, grid, lds, ctx->stream, a, ev0, ev1);
       RM_HIP(ctx, hipGetLastError());
-      if (ev1) RM_HIP(ctx, hipEventRecord(ev1, ctx->stream));
     }
     if (has_bwd) {
       const int nblocks = (int)nb;
