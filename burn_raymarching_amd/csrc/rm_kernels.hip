@@ -21,7 +21,7 @@
 // MFMA fragments (march). The soft-min log-sum-exp runs in base 2 on v_exp_f32/v_log_f32 with
 // the cheapest provably safe shift. Per-sphere gradients are summed over the 64 rays of a
 // wave with a transposing permlane/DPP reduction, over the live waves in LDS, and over
-// workgroups in a fixed order by rm_reduce_partials + rm_finalize_grads (deterministic; no
+// workgroups in a fixed order by rm_reduce_partials (deterministic; no floating-point
 // atomics). DESIGN.md §4 has the details and the measurements.
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
@@ -50,7 +50,7 @@ namespace rm {
 enum Mode { kFwd = 0, kBwd = 1, kTrain = 2, kRender = 3 };
 
 constexpr int kMaxBlocksPerLaunch = 4096; // bounds the partial-gradient workspace per launch
-constexpr int kReduceSegs = 32;           // block segments of the first reduction pass
+constexpr int kReduceSegs = 64;           // block segments of the reduction (<= 256 blocks each)
 
 struct KArgs {
   // rays: array mode (org/dir) or camera mode (cams)
@@ -297,15 +297,19 @@ __device__ void write_bound(const KArgs& a, float* hdr, float* esc) {
     hdr[7] = R;
   }
   if (threadIdx.x < kEscTab) {
+    // f32 with a 1e-5 relative + 1e-6 absolute round-up per iteration (the f32 rounding of one
+    // iteration is a few 1e-7): every T(n) stays above the exact inverse iterate. (R' rounded up
+    // is conservative too: F^-1 grows with R' for y > R', which holds along the table.)
     float tv = INFINITY;
     if (a.gone_d > 0.0f) {
-      const double rp = (double)R + (double)a.lse_slack + 1e-3;
-      double T = (double)a.gone_d + rp;
+      const float rp = (R + a.lse_slack + 1e-3f) * (1.0f + 1e-6f);
+      const float inv_shrink = 1.0000101f;  // > 1 / (1 - 1e-5)
+      float T = (a.gone_d + rp) * (1.0f + 1e-6f);
       for (int n = 1; n <= (int)threadIdx.x; ++n) {
-        const double y = T / (1.0 - 1e-5);
-        T = 0.5 * (rp + sqrt(2.0 * y * y - rp * rp)) * (1.0 + 1e-6) + 1e-6;
+        const float y = T * inv_shrink;
+        T = fmaf(0.5f * (rp + sqrtf(fmaf(2.0f * y, y, -rp * rp))), 1.0f + 1e-5f, 1e-6f);
       }
-      tv = (float)(T * (1.0 + 1e-6));
+      tv = T * (1.0f + 1e-6f);
     }
     esc[threadIdx.x] = tv;
   }
@@ -314,7 +318,25 @@ __device__ void write_bound(const KArgs& a, float* hdr, float* esc) {
 // Records of the call (see Lds), one thread per sphere pair. Each block reduces its pairs'
 // {r_min, r_max, spread} into the header (one block) or its partial (several blocks, then
 // rm_prep_finish); the final header also gets the scene's bounding sphere (scene_bound).
-__global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a, float4* __restrict__ rec) {
+constexpr int kPrepStageMax = 512;  // one-block prep: parameters staged in LDS up to this M
+
+__global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __restrict__ rec) {
+  // One-block case: stage the parameters in LDS once (one load round instead of one per phase:
+  // records, MFMA tiles, header, bounding sphere); the phases below read them through `a`.
+  __shared__ float stage[7 * kPrepStageMax];
+  KArgs a = a0;
+  if (gridDim.x == 1 && a0.M <= kPrepStageMax) {
+    const int M = a0.M;
+    for (int e = threadIdx.x; e < 3 * M; e += 256) {
+      stage[e] = a0.centers[e];
+      stage[3 * M + e] = a0.colors[e];
+    }
+    for (int e = threadIdx.x; e < M; e += 256) stage[6 * M + e] = a0.radius[e];
+    __syncthreads();
+    a.centers = stage;
+    a.colors = stage + 3 * M;
+    a.radius = stage + 6 * M;
+  }
   const int np = a.Mpad / 2;
   float4* P0 = rec;
   float4* P1 = P0 + np;
@@ -851,8 +873,7 @@ __device__ __forceinline__ void escaped_block(const KArgs& a, const Lds& L, long
     a.out[3 * ri + 2] = 0.0f;
   }
   if constexpr (MODE == kFwd || MODE == kRender) return;
-  float* rec = a.partials + blk * a.rec;
-  for (long long e = tid; e < (long long)a.Mpad * 12; e += kBlock) rec[e] = 0.0f;
+  float* rec = a.partials + blk * a.rec;  // per-sphere columns stay unwritten: live flag 0
   float loss = 0.0f;
   if (MODE == kTrain && valid) {  // training.rs:17-34 with out = 0
     const float t0 = a.targets[3 * ri], t1 = a.targets[3 * ri + 1], t2 = a.targets[3 * ri + 2];
@@ -1315,9 +1336,8 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
 #pragma unroll
   for (int w = 0; w < kWaves; ++w) alive |= wflag[w] ? 0 : (1 << w);
   if (dead) {
-    if (alive == 0 && wave == 0) {  // the whole block escaped: zero record + scalar totals
-      for (long long e = lane; e < (long long)a.Mpad * 12; e += 64) rec[e] = 0.0f;
-      if (lane < 8) {
+    if (alive == 0 && wave == 0) {  // the whole block escaped: scalar totals, live flag 0 (the
+      if (lane < 8) {               // reduction skips the per-sphere columns, all zero)
         float acc = wscal[lane];
 #pragma unroll
         for (int w = 1; w < kWaves; ++w) acc += wscal[w * 8 + lane];
@@ -1455,97 +1475,116 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     float acc = wscal[lane];
 #pragma unroll
     for (int w = 1; w < kWaves; ++w) acc += wscal[w * 8 + lane];
-    rec[(long long)a.Mpad * 12 + lane] = acc;
+    rec[(long long)a.Mpad * 12 + lane] = lane == 7 ? 1.0f : acc;  // scalar 7: live flag
   }
 }
 
 // ---- cross-block reduction (fixed order => deterministic) --------------------------------
 // Partial record of one ray block (rec = Mpad*12 + 8 floats):
 //   [Mpad][8] sweep 1 (gc.xyz, gr, gcol.rgb, 0) | [Mpad][4] sweep 2 (gc.xyz, gr) | 8 scalars
+// Scalar 7 is the block's live flag: 0 when every wave of the block left the march early (its
+// per-sphere columns are all zero and were not written), 1 otherwise.
 // Output columns (ncols = Mpad*8 + 8): [Mpad][8] combined per-sphere grads | 8 scalars.
-// Pass 1: S[seg][col] = sum over blocks of segment seg (sweep-2 terms folded into their column).
-// Four independent accumulators keep four loads in flight per thread; their combine order is
-// fixed, so results stay bitwise reproducible.
-__global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restrict__ P, long long rec, int Mpad,
+//
+// Pass 1, grid (column blocks x segments of ray blocks): each block sums its segment for its 256
+// columns into S[seg][col] -- one addition chain per column in ray-block order (sweep-2 terms
+// added right after their row's sweep-1 term), loads batched eight rows at a time. Rows of dead
+// blocks are skipped: they only hold zeros, and adding +0 leaves a chain unchanged, so the sums
+// are those of the full chain.
+struct FinalArgs {
+  const float* light_dir;
+  float *gc, *gcol, *gr, *gld, *gamb, *loss_sum;
+  int accumulate;
+};
+
+constexpr int kReduceBatch = 8;
+
+__global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restrict__ P, long long rec, int M, int Mpad,
                                                           int nblocks, int seg_len, float* __restrict__ S) {
+  __shared__ int rows[256];
+  __shared__ int wcount[4];
   const int ncols = Mpad * 8 + 8;
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= ncols) return;
-  long long c1, c2 = -1;
-  if (col < Mpad * 8) {
-    c1 = col;
-    const int j = col >> 3, comp = col & 7;
-    if (comp < 4) c2 = (long long)Mpad * 8 + (long long)j * 4 + comp;
-  } else {
-    c1 = (long long)Mpad * 12 + (col - Mpad * 8);
-  }
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = blockIdx.x * 256 + tid;
+  const bool scalars = (int)blockIdx.x * 256 >= Mpad * 8;  // the column block of the 8 scalars
   const int b0 = blockIdx.y * seg_len;
   const int b1 = min(b0 + seg_len, nblocks);
-  float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
-  int b = b0;
-  if (c2 >= 0) {
-    for (; b + 1 < b1; b += 2) {
-      const float* r0 = P + (long long)b * rec;
-      const float* r1 = r0 + rec;
-      a0 += r0[c1];
-      a1 += r0[c2];
-      a2 += r1[c1];
-      a3 += r1[c2];
-    }
-    for (; b < b1; ++b) {
-      a0 += P[(long long)b * rec + c1];
-      a1 += P[(long long)b * rec + c2];
-    }
-  } else {
-    for (; b + 3 < b1; b += 4) {
-      const float* r0 = P + (long long)b * rec + c1;
-      a0 += r0[0];
-      a1 += r0[rec];
-      a2 += r0[2 * rec];
-      a3 += r0[3 * rec];
-    }
-    for (; b < b1; ++b) a0 += P[(long long)b * rec + c1];
+  // rows of this segment to visit, in order: every row for the scalars, live rows otherwise
+  {
+    const int b = b0 + tid;
+    const bool take = b < b1 && (scalars || P[(long long)b * rec + (long long)Mpad * 12 + 7] != 0.0f);
+    const unsigned long long m = __ballot(take);
+    if (lane == 0) wcount[wave] = __popcll(m);
+    __syncthreads();
+    int base = 0;
+    for (int w = 0; w < wave; ++w) base += wcount[w];
+    if (take) rows[base + __popcll(m & ((1ull << lane) - 1))] = b;
+    __syncthreads();
   }
-  S[(long long)blockIdx.y * ncols + col] = (a0 + a1) + (a2 + a3);
+  const int nrows = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+  if (col < ncols) {
+    long long c1, c2 = -1;
+    if (col < Mpad * 8) {
+      c1 = col;
+      const int j = col >> 3, comp = col & 7;
+      if (comp < 4) c2 = (long long)Mpad * 8 + (long long)j * 4 + comp;
+    } else {
+      c1 = (long long)Mpad * 12 + (col - Mpad * 8);
+    }
+    float acc = 0.0f;
+    for (int i0 = 0; i0 < nrows; i0 += kReduceBatch) {
+      float v1[kReduceBatch], v2[kReduceBatch];
+#pragma unroll
+      for (int u = 0; u < kReduceBatch; ++u) {
+        const int i = min(i0 + u, nrows - 1);
+        const float* r = P + (long long)rows[i] * rec;
+        v1[u] = r[c1];
+        v2[u] = c2 >= 0 ? r[c2] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < kReduceBatch; ++u)
+        if (i0 + u < nrows) {
+          acc += v1[u];
+          if (c2 >= 0) acc += v2[u];
+        }
+    }
+    S[(long long)blockIdx.y * ncols + col] = acc;
+  }
 }
 
-// Pass 2: sum the segments in order and scatter into the caller's gradient layout.
+// Pass 2: sum the segments in order and scatter into the caller's gradient layout (a separate
+// launch: the kernel boundary makes pass 1's sums visible across the XCDs' L2s, which a
+// device-scope fence per block would do at the cost of an L2 writeback each).
 // gld = (g_ell - ldn (ldn . g_ell)) / |ld| applies the Jacobian of ld / |ld| (renderer_diff.rs:49-50).
-__device__ __forceinline__ float sum_segments(const float* __restrict__ S, int ncols, int nseg, int col) {
-  float a0 = 0.0f, a1 = 0.0f, a2 = 0.0f, a3 = 0.0f;
-  int s = 0;
-  for (; s + 3 < nseg; s += 4) {
-    const float* r = S + (long long)s * ncols + col;
-    a0 += r[0];
-    a1 += r[ncols];
-    a2 += r[2 * ncols];
-    a3 += r[3 * ncols];
-  }
-  for (; s < nseg; ++s) a0 += S[(long long)s * ncols + col];
-  return (a0 + a1) + (a2 + a3);
-}
-
 __global__ __launch_bounds__(256) void rm_finalize_grads(const float* __restrict__ S, int nseg, int M, int Mpad,
-                                                         const float* __restrict__ light_dir, float* gc,
-                                                         float* gcol, float* gr, float* gld, float* gamb,
-                                                         float* loss_sum, int accumulate) {
+                                                         FinalArgs f) {
   const int ncols = Mpad * 8 + 8;
   const int col = blockIdx.x * 256 + threadIdx.x;
+  (void)nseg;  // == kReduceSegs always (pass 1 writes every segment, empty ones as 0): all loads in
+  // flight, then four chains s mod 4 combined in a fixed order
+  auto seg_sum = [&](int c) {
+    float v[kReduceSegs];
+#pragma unroll
+    for (int s = 0; s < kReduceSegs; ++s) v[s] = S[(long long)s * ncols + c];
+    float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int s = 0; s < kReduceSegs; ++s) a[s & 3] += v[s];
+    return (a[0] + a[1]) + (a[2] + a[3]);
+  };
   if (col >= ncols) return;
   if (col < Mpad * 8) {
     const int j = col >> 3, comp = col & 7;
     if (j >= M || comp == 7) return;
-    const float v = sum_segments(S, ncols, nseg, col);
-    float* dst = comp < 3 ? (gc ? gc + 3 * j + comp : nullptr)
-                          : (comp == 3 ? (gr ? gr + j : nullptr) : (gcol ? gcol + 3 * j + (comp - 4) : nullptr));
-    if (dst) *dst = accumulate ? *dst + v : v;
+    const float v = seg_sum(col);
+    float* dst = comp < 3 ? (f.gc ? f.gc + 3 * j + comp : nullptr)
+                          : (comp == 3 ? (f.gr ? f.gr + j : nullptr) : (f.gcol ? f.gcol + 3 * j + (comp - 4) : nullptr));
+    if (dst) *dst = f.accumulate ? *dst + v : v;
     return;
   }
   const int sc = col - Mpad * 8;
-  if (sc == 0 && gld) {
-    const float r0 = sum_segments(S, ncols, nseg, col), r1 = sum_segments(S, ncols, nseg, col + 1),
-                r2 = sum_segments(S, ncols, nseg, col + 2);
-    const float l0 = light_dir[0], l1 = light_dir[1], l2 = light_dir[2];
+  if (sc == 0 && f.gld) {
+    const float r0 = seg_sum(col), r1 = seg_sum(col + 1), r2 = seg_sum(col + 2);
+    const float l0 = f.light_dir[0], l1 = f.light_dir[1], l2 = f.light_dir[2];
     const float len = sqrtf(l0 * l0 + l1 * l1 + l2 * l2);
     const float ln[3] = {l0 / len, l1 / len, l2 / len};
     const float r[3] = {r0, r1, r2};
@@ -1553,14 +1592,14 @@ __global__ __launch_bounds__(256) void rm_finalize_grads(const float* __restrict
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
       const float gv = (r[c] - ln[c] * proj) / len;
-      gld[c] = accumulate ? gld[c] + gv : gv;
+      f.gld[c] = f.accumulate ? f.gld[c] + gv : gv;
     }
-  } else if (sc == 3 && gamb) {
-    const float v = sum_segments(S, ncols, nseg, col);
-    gamb[0] = accumulate ? gamb[0] + v : v;
-  } else if (sc == 4 && loss_sum) {
-    const float v = sum_segments(S, ncols, nseg, col);
-    loss_sum[0] = accumulate ? loss_sum[0] + v : v;
+  } else if (sc == 3 && f.gamb) {
+    const float v = seg_sum(col);
+    f.gamb[0] = f.accumulate ? f.gamb[0] + v : v;
+  } else if (sc == 4 && f.loss_sum) {
+    const float v = seg_sum(col);
+    f.loss_sum[0] = f.accumulate ? f.loss_sum[0] + v : v;
   }
 }
 
@@ -2098,22 +2137,23 @@ int run(rm_context* ctx, const Call& c) {
       const int nblocks = (int)nb;
       const int ncols = Mpad * 8 + 8;
       float* S = P + (long long)std::max<long long>(nb, 1) * a.rec;
-      int segs = std::min(kReduceSegs, std::max(nblocks, 1));
-      const int seg_len = nblocks > 0 ? (nblocks + segs - 1) / segs : 0;
-      if (nblocks > 0) segs = (nblocks + seg_len - 1) / seg_len;
-      if (nblocks > 0) {
-        dim3 g1((unsigned)((ncols + 255) / 256), (unsigned)segs);
-        hipLaunchKernelGGL(rm_reduce_partials, g1, dim3(256), 0, ctx->stream, P, a.rec, Mpad, nblocks, seg_len, S);
-        RM_HIP(ctx, hipGetLastError());
-      } else {
-        RM_HIP(ctx, hipMemsetAsync(S, 0, sizeof(float) * ncols, ctx->stream));
-        segs = 1;
-      }
+      const int segs = kReduceSegs;  // every segment is written (empty ones as 0)
+      const int seg_len = (nblocks + segs - 1) / segs;
+      const int xblocks = (ncols + 255) / 256;
       const rm_grads* gp = c.grads;
-      const int acc = (first ? c.accumulate : 1);
-      hipLaunchKernelGGL(rm_finalize_grads, dim3((ncols + 255) / 256), dim3(256), 0, ctx->stream, S, segs, M, Mpad,
-                         c.scene->light_dir, gp->centers, gp->colors, gp->radius, gp->light_dir, gp->ambient,
-                         c.mode == kTrain ? c.loss_sum : nullptr, acc);
+      FinalArgs fa;
+      fa.light_dir = c.scene->light_dir;
+      fa.gc = gp->centers;
+      fa.gcol = gp->colors;
+      fa.gr = gp->radius;
+      fa.gld = gp->light_dir;
+      fa.gamb = gp->ambient;
+      fa.loss_sum = c.mode == kTrain ? c.loss_sum : nullptr;
+      fa.accumulate = first ? c.accumulate : 1;
+      hipLaunchKernelGGL(rm_reduce_partials, dim3((unsigned)xblocks, (unsigned)segs), dim3(256), 0, ctx->stream, P,
+                         a.rec, M, Mpad, nblocks, seg_len, S);
+      RM_HIP(ctx, hipGetLastError());
+      hipLaunchKernelGGL(rm_finalize_grads, dim3((unsigned)xblocks), dim3(256), 0, ctx->stream, S, segs, M, Mpad, fa);
       RM_HIP(ctx, hipGetLastError());
     }
     done += nr;
