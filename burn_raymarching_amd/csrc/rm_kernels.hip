@@ -399,14 +399,18 @@ __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __
   char* tiles = reinterpret_cast<char*>(rec) + tiles_offset(np, gridDim.x);
   uint4* At = reinterpret_cast<uint4*>(tiles);
   float* Wt = reinterpret_cast<float*>(At + (size_t)nrb * 64);
+#ifndef RM_DBG_NO_TILES
   for (int e = blockIdx.x * 256 + threadIdx.x; e < nrb * 64; e += gridDim.x * 256) At[e] = mfma_a_frag(a, e >> 6, e & 63);
+#endif
   for (int e = blockIdx.x * 256 + threadIdx.x; e < nrb * 32; e += gridDim.x * 256) {
     const int j = 16 * (e >> 5) + (e & 15);
     const float krj = j < a.M ? kappa * a.radius[j] : 0.0f;
     Wt[e] = j >= a.M ? 0.0f : ((e & 16) ? fexp2(krj - kr_first) : fexp2(krj));
   }
   header_reduce(rmin, rmax, spread, gridDim.x == 1 ? hdr : hdr + (size_t)(1 + blockIdx.x) * kRecHeader);
+#ifndef RM_DBG_NO_BOUND
   if (gridDim.x == 1) write_bound(a, hdr, reinterpret_cast<float*>(reinterpret_cast<char*>(rec) + esc_offset(np, 1)));
+#endif
 }
 
 __global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, float* __restrict__ hdr, float* __restrict__ esc,
