@@ -223,7 +223,7 @@ __device__ __forceinline__ void scene_bound(const KArgs& a, float* scratch, int 
   float r = 0.0f;
   for (int j = tid; j < a.M; j += kBlock) {
     const float dx = a.centers[3 * j] - c0[0], dy = a.centers[3 * j + 1] - c0[1], dz = a.centers[3 * j + 2] - c0[2];
-    r = fmaxf(r, sqrtf(dx * dx + dy * dy + dz * dz) + a.radius[j]);
+    r = fmaxf(r, fsqrt(dx * dx + dy * dy + dz * dz) + a.radius[j]);  // 1 ulp: inside the round-up below
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) r = fmaxf(r, __shfl_xor(r, off));
@@ -303,12 +303,12 @@ __device__ void write_bound(const KArgs& a, float* hdr, float* esc) {
     float tv = INFINITY;
     if (a.gone_d > 0.0f) {
       const float rp = (R + a.lse_slack + 1e-3f) * (1.0f + 1e-6f);
-      const float inv_shrink = 1.0000101f;  // > 1 / (1 - 1e-5)
+      const float inv_shrink = 1.0000101f;  // y = T / (1 - 1e-5) <= T inv_shrink
       float T = (a.gone_d + rp) * (1.0f + 1e-6f);
-      for (int n = 1; n <= (int)threadIdx.x; ++n) {
-        const float y = T * inv_shrink;
-        T = fmaf(0.5f * (rp + sqrtf(fmaf(2.0f * y, y, -rp * rp))), 1.0f + 1e-5f, 1e-6f);
-      }
+      // four dependent instructions per step (v_sqrt_f32: 1 ulp, inside the round-up)
+      const float two_c2 = 2.0f * inv_shrink * inv_shrink * (1.0f + 1e-6f), nrp2 = -rp * rp,
+                  half_up = 0.5f * (1.0f + 1e-5f);
+      for (int n = 1; n <= (int)threadIdx.x; ++n) T = fmaf(rp + fsqrt(fmaf(two_c2 * T, T, nrp2)), half_up, 1e-6f);
       tv = T * (1.0f + 1e-6f);
     }
     esc[threadIdx.x] = tv;
