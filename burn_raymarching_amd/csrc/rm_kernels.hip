@@ -860,8 +860,15 @@ __device__ __forceinline__ bool escapes(const float o[3], const float d[3], floa
 // machine while the heavy blocks finish. Partials stay indexed by the logical block, so the
 // gradient sums (and every result) do not depend on the order.
 __device__ __forceinline__ long long ray_block(const KArgs& a) {
-  const int b = blockIdx.x;
+  int b = blockIdx.x;
   if (a.block_order == nullptr) return b;
+  // The dispatcher hands block i to XCD i % 8. With the views interleaved (b = rank * V + v),
+  // V = 2 or 4 would pin each view to a fixed subset of XCDs, and views differ in cost (how much
+  // of the scene they see): the XCDs of the dearest view finish last. Rotating the positions
+  // inside every full round of 8 blocks by the round number makes each XCD cycle through all
+  // views (rank order is kept up to 8 positions, so heavy tiles still start first).
+  const int g = b >> 3;
+  if ((g + 1) * 8 <= (int)gridDim.x) b = (g << 3) + (((b & 7) + g) & 7);
   const int r = b / a.order_views, v = b - r * a.order_views;
   return (long long)v * a.order_tiles + a.block_order[r];
 }
