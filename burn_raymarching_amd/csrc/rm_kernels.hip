@@ -43,6 +43,9 @@
 #ifndef RM_PRIO_RAMP
 #define RM_PRIO_RAMP 1
 #endif
+#ifndef RM_BWD_TRANSPOSED
+#define RM_BWD_TRANSPOSED 1  // backward sweeps with one sphere per lane (0: one ray per lane)
+#endif
 
 namespace rm {
 
@@ -154,9 +157,13 @@ struct Lds {  // the sphere records (global, scalar-loaded) plus the kernel's LD
 
 // LDS: the backward's two partial buffers, or (during the march) lse_mfma's per-wave ray
 // exchange (64 x (16 + 16 + 4) B per wave); then 256 B of misc scratch.
-constexpr size_t kSlotBytes = (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float) > (size_t)kWaves * 64 * 36
-                                  ? (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float)
-                                  : (size_t)kWaves * 64 * 36;
+// The transposed backward (RM_BWD_TRANSPOSED) uses 2 x kWaves x 8 x 64 combine floats, 64 x 12
+// ray-data floats and 64 x 4 g_p floats per wave.
+constexpr size_t kSlotBwdT = ((size_t)2 * kWaves * 8 * 64 + (size_t)kWaves * 64 * 16) * sizeof(float);
+constexpr size_t kSlotBytes0 = (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float) > (size_t)kWaves * 64 * 36
+                                   ? (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float)
+                                   : (size_t)kWaves * 64 * 36;
+constexpr size_t kSlotBytes = RM_BWD_TRANSPOSED && kSlotBwdT > kSlotBytes0 ? kSlotBwdT : kSlotBytes0;
 __host__ __device__ constexpr size_t lds_bytes() { return kSlotBytes + 256; }
 
 // three-value block reduction (min, max, max) for the record header
@@ -1372,6 +1379,233 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     return acc;
   };
 
+#if RM_BWD_TRANSPOSED
+  // ---- backward sweeps with one sphere per lane (transposed). The per-sphere gradient sums
+  // over the wave's rays accumulate in each lane's registers (no cross-lane reduction); the
+  // rays are visited one pair per packed instruction, their data broadcast from LDS. Only the
+  // position gradient g_p of sweep 1 is a per-ray sum over spheres: it is reduced across the
+  // lanes for batches of 8 rays (three transposing reductions) and accumulated in LDS over the
+  // sphere groups. Rays whose seeds are zero contribute exact zeros and are skipped (sweep 1:
+  // gm = 0 and b_scale = 0; sweep 2: g_t = 0) -- in practice the escaped rays of live waves.
+  // Distances are formed with the same fp32 operations and operands as the forward sweeps
+  // (qpair), so dd = dmin - delta <= 0 and v - mA <= 0 hold exactly, as in the lane=ray form.
+  {
+    (void)slots;
+    float* comb = L.slots;  // [2][kWaves][8][64] per-sphere wave sums (double-buffered)
+    float4* rayd = reinterpret_cast<float4*>(L.slots + 2 * kWaves * 8 * 64) + wave * 64 * 3;
+    float* gpa = L.slots + 2 * kWaves * 8 * 64 + kWaves * 64 * 12 + wave * 64 * 4;
+    const int np = a.Mpad / 2;
+    const float4* R4 = reinterpret_cast<const float4*>(a.rec_buf);
+    const float2* R2 = reinterpret_cast<const float2*>(R4 + 7 * (size_t)np);
+    const int ngrp = (a.Mpad + 63) / 64;
+    // the block's live waves sum their per-sphere lane sums in wave order into the record
+    auto combine = [&](const float (&v)[8], int ncomp, long long rec_base, int grp) {
+      float* cb = comb + (chunk_ctr & 1) * (kWaves * 8 * 64);
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        if (c < ncomp) cb[(wave * 8 + c) * 64 + lane] = v[c];
+      __syncthreads();
+      for (int e = atid; e < 64 * ncomp; e += astride) {
+        const int sl = e / ncomp, c = e - sl * ncomp;
+        if (grp * 64 + sl < a.Mpad) rec[rec_base + (long long)(grp * 64 + sl) * ncomp + c] = live_sum(cb + c * 64 + sl, 8 * 64);
+      }
+      ++chunk_ctr;
+    };
+    // up to 8 active rays of mask m (lowest first) into idx; returns their count
+    auto take8 = [&](unsigned long long& m, int (&idx)[8]) {
+      int nb = 0;
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        if (m != 0ull) {
+          idx[u] = __builtin_ctzll(m);
+          m &= m - 1ull;
+          ++nb;
+        } else {
+          idx[u] = idx[0];
+        }
+      }
+      return nb;
+    };
+
+    // ---- sweep 1 at p_final: colour softmax + mask soft-min + p_final(t_final)
+    rayd[lane * 3 + 0] = make_float4(p[0], p[1], p[2], psq(p));
+    rayd[lane * 3 + 1] = make_float4(dmin, invZw, b_scale, mg);
+    rayd[lane * 3 + 2] = make_float4(gm[0], gm[1], gm[2], 0.0f);
+    gpa[lane * 4 + 0] = 0.0f;
+    gpa[lane * 4 + 1] = 0.0f;
+    gpa[lane * 4 + 2] = 0.0f;
+    const unsigned long long act1 = __ballot(gm[0] != 0.0f || gm[1] != 0.0f || gm[2] != 0.0f || b_scale != 0.0f);
+    __builtin_amdgcn_wave_barrier();
+    {
+      const f2 CL = sp(c10l), KA = sp(kappa), NCS = sp(-a.csharp);
+      auto sweep1 = [&](auto clamp_tag) {
+        constexpr bool CLAMP = decltype(clamp_tag)::value;
+        for (int grp = 0; grp < ngrp; ++grp) {
+          const int j = grp * 64 + lane;
+          float gx = -2.0f * kPadCenter, gy = 0.0f, gz = 0.0f, cc = kPadCenter * kPadCenter, rr = 0.0f, cr = 0.0f,
+                cg = 0.0f, cbl = 0.0f;
+          if (j < a.Mpad) {  // sphere j of pair j/2 (records of rm_prep_kernel)
+            const int i = j >> 1;
+            const bool h = (j & 1) != 0;
+            const float4 A = R4[i], B = R4[np + i], R = R4[2 * np + i], C3 = R4[3 * np + i];
+            const float2 C4 = R2[i];
+            gx = h ? A.y : A.x;
+            gy = h ? A.w : A.z;
+            gz = h ? B.y : B.x;
+            cc = h ? B.w : B.z;
+            rr = h ? R.w : R.z;
+            cr = h ? C3.y : C3.x;
+            cg = h ? C3.w : C3.z;
+            cbl = h ? C4.y : C4.x;
+          }
+          const f2 GX = sp(gx), GY = sp(gy), GZ = sp(gz), CC = sp(cc), RR = sp(rr), CR = sp(cr), CG = sp(cg),
+                   CB = sp(cbl), HX = sp(0.5f * gx), HY = sp(0.5f * gy), HZ = sp(0.5f * gz);
+          f2 agc[3] = {sp(0.0f), sp(0.0f), sp(0.0f)}, agr = sp(0.0f), acol[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
+          unsigned long long m = act1;
+          while (m != 0ull) {
+            int idx[8];
+            const int nb = take8(m, idx);
+            float gpv[3][8];
+#pragma unroll
+            for (int u = 0; u < 8; u += 2) {
+              if (u >= nb) {  // batch slots past the last active ray
+#pragma unroll
+                for (int c = 0; c < 3; ++c) gpv[c][u] = gpv[c][u + 1] = 0.0f;
+                continue;
+              }
+              const float4 a0 = rayd[idx[u] * 3], a1 = rayd[idx[u + 1] * 3];
+              const float4 b0 = rayd[idx[u] * 3 + 1], c0 = rayd[idx[u] * 3 + 2];
+              float4 b1 = rayd[idx[u + 1] * 3 + 1], c1 = rayd[idx[u + 1] * 3 + 2];
+              if (u + 1 >= nb) {  // odd count: the second slot repeats a ray with zero seeds (zero terms)
+                b1.y = b1.z = b1.w = 0.0f;
+                c1 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+              }
+              const f2 PX = f2{a0.x, a1.x}, PY = f2{a0.y, a1.y}, PZ = f2{a0.z, a1.z}, PP = f2{a0.w, a1.w};
+              const f2 DM = f2{b0.x, b1.x}, IZ = f2{b0.y, b1.y}, BS = f2{b0.z, b1.z}, MG = f2{b0.w, b1.w};
+              const f2 G0 = f2{c0.x, c1.x}, G1 = f2{c0.y, c1.y}, G2 = f2{c0.z, c1.z};
+              f2 q = fma2(PZ, GZ, fma2(PY, GY, fma2(PX, GX, PP + CC)));  // == qpair: the shade sweep's q
+              const f2 qraw = q;
+              if constexpr (CLAMP) q = clamp_q(q);
+              const f2 rho = sqrt2(q);
+              const f2 dl = rho - RR;
+              const f2 ir = rcp2(rho);
+              const f2 dd = DM - dl;  // <= 0 exactly
+              const f2 w = exp2v(dd * CL) * IZ;
+              const f2 bt = exp2v(dd * KA) * BS;
+              const f2 cgm = fma2(CB, G2, fma2(CG, G1, CR * G0));
+              const f2 gd = fma2(w * NCS, cgm - MG, bt);
+              f2 gu = gd * ir;
+              if constexpr (CLAMP) {  // clamp_min(1e-6) gate
+                gu.x = qraw.x >= 1e-6f ? gu.x : 0.0f;
+                gu.y = qraw.y >= 1e-6f ? gu.y : 0.0f;
+              }
+              const f2 ex = HX + PX, ey = HY + PY, ez = HZ + PZ;  // == fma2(HALF, -2c, p) = p - c
+              const f2 px = gu * ex, py = gu * ey, pz = gu * ez;
+              gpv[0][u] = px.x;
+              gpv[0][u + 1] = px.y;
+              gpv[1][u] = py.x;
+              gpv[1][u + 1] = py.y;
+              gpv[2][u] = pz.x;
+              gpv[2][u + 1] = pz.y;
+              agc[0] -= px;
+              agc[1] -= py;
+              agc[2] -= pz;
+              agr -= gd;
+              acol[0] = fma2(w, G0, acol[0]);
+              acol[1] = fma2(w, G1, acol[1]);
+              acol[2] = fma2(w, G2, acol[2]);
+            }
+            const float r0 = wave_reduce8(gpv[0], lane), r1 = wave_reduce8(gpv[1], lane), r2 = wave_reduce8(gpv[2], lane);
+            if ((lane & 7) == 7) {
+              const int k = lane >> 3;
+              int n = idx[0];
+#pragma unroll
+              for (int u = 1; u < 8; ++u) n = k == u ? idx[u] : n;
+              if (k < nb) {
+                gpa[n * 4 + 0] += r0;
+                gpa[n * 4 + 1] += r1;
+                gpa[n * 4 + 2] += r2;
+              }
+            }
+          }
+          const float v[8] = {agc[0].x + agc[0].y, agc[1].x + agc[1].y, agc[2].x + agc[2].y, agr.x + agr.y,
+                              acol[0].x + acol[0].y, acol[1].x + acol[1].y, acol[2].x + acol[2].y, 0.0f};
+          combine(v, 8, 0, grp);
+        }
+      };
+      if (fast_f) sweep1(std::false_type{});
+      else sweep1(std::true_type{});
+    }
+
+    // ---- sweep 2 at p_approx: t_final = t + D(p_approx) -> g_t * softmax(-k dist_a)
+    __builtin_amdgcn_wave_barrier();
+    const float gt = fmaf(gpa[lane * 4 + 2], d[2], fmaf(gpa[lane * 4 + 1], d[1], gpa[lane * 4] * d[0]));
+    const float hs = gt * frcp(sA);
+    __syncthreads();  // every wave is done reading the sweep-1 ray data and combine buffers
+    rayd[lane * 3 + 0] = make_float4(pa[0], pa[1], pa[2], psq(pa));
+    rayd[lane * 3 + 1] = make_float4(mA, hs, 0.0f, 0.0f);
+    const unsigned long long act2 = __ballot(hs != 0.0f);
+    __builtin_amdgcn_wave_barrier();
+    {
+      const f2 NK = sp(nkappa);
+      auto sweep2 = [&](auto clamp_tag) {
+        constexpr bool CLAMP = decltype(clamp_tag)::value;
+        for (int grp = 0; grp < ngrp; ++grp) {
+          const int j = grp * 64 + lane;
+          float gx = -2.0f * kPadCenter, gy = 0.0f, gz = 0.0f, cc = kPadCenter * kPadCenter, kr = 0.0f;
+          if (j < a.Mpad) {
+            const int i = j >> 1;
+            const bool h = (j & 1) != 0;
+            const float4 A = R4[i], B = R4[np + i], R = R4[2 * np + i];
+            gx = h ? A.y : A.x;
+            gy = h ? A.w : A.z;
+            gz = h ? B.y : B.x;
+            cc = h ? B.w : B.z;
+            kr = h ? R.y : R.x;
+          }
+          const f2 GX = sp(gx), GY = sp(gy), GZ = sp(gz), CC = sp(cc), KR = sp(kr), HX = sp(0.5f * gx),
+                   HY = sp(0.5f * gy), HZ = sp(0.5f * gz);
+          f2 agc[3] = {sp(0.0f), sp(0.0f), sp(0.0f)}, agr = sp(0.0f);
+          unsigned long long m = act2;
+          while (m != 0ull) {
+            int idx[8];
+            const int nb = take8(m, idx);
+#pragma unroll
+            for (int u = 0; u < 8; u += 2) {
+              if (u >= nb) break;
+              const float4 a0 = rayd[idx[u] * 3], a1 = rayd[idx[u + 1] * 3];
+              const float4 b0 = rayd[idx[u] * 3 + 1];
+              float4 b1 = rayd[idx[u + 1] * 3 + 1];
+              if (u + 1 >= nb) b1.y = 0.0f;
+              const f2 PX = f2{a0.x, a1.x}, PY = f2{a0.y, a1.y}, PZ = f2{a0.z, a1.z}, PP = f2{a0.w, a1.w};
+              const f2 MA = f2{b0.x, b1.x}, HS = f2{b0.y, b1.y};
+              f2 q = fma2(PZ, GZ, fma2(PY, GY, fma2(PX, GX, PP + CC)));  // == qpair: the reconnect sweep's q
+              const f2 qraw = q;
+              if constexpr (CLAMP) q = clamp_q(q);
+              const f2 rho = sqrt2(q);
+              const f2 h = exp2v(fma2(rho, NK, KR) - MA) * HS;  // v - mA <= 0 exactly
+              f2 hu = h * rcp2(rho);
+              if constexpr (CLAMP) {
+                hu.x = qraw.x >= 1e-6f ? hu.x : 0.0f;
+                hu.y = qraw.y >= 1e-6f ? hu.y : 0.0f;
+              }
+              agc[0] = fma2(-hu, HX + PX, agc[0]);
+              agc[1] = fma2(-hu, HY + PY, agc[1]);
+              agc[2] = fma2(-hu, HZ + PZ, agc[2]);
+              agr -= h;
+            }
+          }
+          const float v[8] = {agc[0].x + agc[0].y, agc[1].x + agc[1].y, agc[2].x + agc[2].y, agr.x + agr.y,
+                              0.0f, 0.0f, 0.0f, 0.0f};
+          combine(v, 4, (long long)a.Mpad * 8, grp);
+        }
+      };
+      if (fast_a) sweep2(std::false_type{});
+      else sweep2(std::true_type{});
+    }
+  }
+  __syncthreads();
+#else
   // ---- backward sweep 1 at p_final: colour softmax + mask soft-min + p_final(t_final)
   f2 GP[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
   {
@@ -1480,6 +1714,8 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
       for_tiles([&](int t0, int tn) { sweep2(std::true_type{}, t0, tn); });
   }
   __syncthreads();
+
+#endif  // RM_BWD_TRANSPOSED
 
   // ---- per-ray scalar totals of the block (published before the sweeps)
   if (arank == 0 && lane < 8) {
