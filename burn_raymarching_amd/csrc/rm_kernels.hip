@@ -46,6 +46,9 @@
 #ifndef RM_BWD_TRANSPOSED
 #define RM_BWD_TRANSPOSED 1  // backward sweeps with one sphere per lane (0: one ray per lane)
 #endif
+#ifndef RM_BWD_COMB_BUFS
+#define RM_BWD_COMB_BUFS 1  // transposed backward: combine buffers (1 keeps the block's LDS <= 32 KB)
+#endif
 
 namespace rm {
 
@@ -81,6 +84,7 @@ struct KArgs {
   const float* ambient;
   int M, Mpad;
   const float4* rec_buf;  // sphere records of this call (rm_prep_kernel), see Lds
+  float* origin;  // camera mode, nullable: per view, the first march step's D at the eye (write_origins)
   // march / shading
   int steps;
   float k, eps, csharp, msharp;
@@ -129,8 +133,12 @@ __host__ __device__ inline size_t esc_offset(int npairs, int nprep) {
   const size_t nrb = (size_t)npairs / 8;
   return tiles_offset(npairs, nprep) + nrb * 64 * 16 + nrb * 32 * sizeof(float);
 }
-__host__ __device__ inline size_t rec_bytes(int npairs, int nprep) {
+// Then the per-view origin steps of camera mode (write_origins): RM_MAX_VIEWS_PER_CALL floats.
+__host__ __device__ inline size_t origin_offset(int npairs, int nprep) {
   return esc_offset(npairs, nprep) + kEscTab * sizeof(float);
+}
+__host__ __device__ inline size_t rec_bytes(int npairs, int nprep) {
+  return origin_offset(npairs, nprep) + RM_MAX_VIEWS_PER_CALL * sizeof(float);
 }
 
 struct Lds {  // the sphere records (global, scalar-loaded) plus the kernel's LDS scratch
@@ -157,9 +165,12 @@ struct Lds {  // the sphere records (global, scalar-loaded) plus the kernel's LD
 
 // LDS: the backward's two partial buffers, or (during the march) lse_mfma's per-wave ray
 // exchange (64 x (16 + 16 + 4) B per wave); then 256 B of misc scratch.
-// The transposed backward (RM_BWD_TRANSPOSED) uses 2 x kWaves x 8 x 64 combine floats, 64 x 12
-// ray-data floats and 64 x 4 g_p floats per wave.
-constexpr size_t kSlotBwdT = ((size_t)2 * kWaves * 8 * 64 + (size_t)kWaves * 64 * 16) * sizeof(float);
+// The transposed backward (RM_BWD_TRANSPOSED) uses RM_BWD_COMB_BUFS x kWaves x 8 x 64 combine
+// floats, 64 x 12 ray-data floats and 64 x 4 g_p floats per wave. The LDS of a block decides how
+// many blocks a CU holds once waves leave the march early (their registers free up, the block's
+// LDS stays until its last wave ends): 24.3 KB -> 6 blocks per CU, 32.3 KB -> 4.
+constexpr size_t kSlotBwdT =
+    ((size_t)RM_BWD_COMB_BUFS * kWaves * 8 * 64 + (size_t)kWaves * 64 * 16) * sizeof(float);
 constexpr size_t kSlotBytes0 = (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float) > (size_t)kWaves * 64 * 36
                                    ? (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float)
                                    : (size_t)kWaves * 64 * 36;
@@ -327,10 +338,13 @@ __device__ void write_bound(const KArgs& a, float* hdr, float* esc) {
 // rm_prep_finish); the final header also gets the scene's bounding sphere (scene_bound).
 constexpr int kPrepStageMax = 512;  // one-block prep: parameters staged in LDS up to this M
 
+__device__ void write_origins(const KArgs& a, const float4* rec, const float* hdr, float* orig, unsigned char* xch);
+
 __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __restrict__ rec) {
   // One-block case: stage the parameters in LDS once (one load round instead of one per phase:
   // records, MFMA tiles, header, bounding sphere); the phases below read them through `a`.
   __shared__ float stage[7 * kPrepStageMax];
+  __shared__ __attribute__((aligned(16))) unsigned char oxch[kWaves * 64 * 36];  // write_origins' ray exchange
   KArgs a = a0;
   if (gridDim.x == 1 && a0.M <= kPrepStageMax) {
     const int M = a0.M;
@@ -418,10 +432,16 @@ __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __
 #ifndef RM_DBG_NO_BOUND
   if (gridDim.x == 1) write_bound(a, hdr, reinterpret_cast<float*>(reinterpret_cast<char*>(rec) + esc_offset(np, 1)));
 #endif
+  if (gridDim.x == 1 && a.origin != nullptr) {
+    __threadfence();
+    __syncthreads();  // the records, tiles and header written above are complete and visible
+    write_origins(a, rec, hdr, a.origin, oxch);
+  }
 }
 
-__global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, float* __restrict__ hdr, float* __restrict__ esc,
-                                                      int nprep) {
+__global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, const float4* __restrict__ rec,
+                                                      float* __restrict__ hdr, float* __restrict__ esc, int nprep) {
+  __shared__ __attribute__((aligned(16))) unsigned char oxch[kWaves * 64 * 36];
   float rmin = INFINITY, rmax = 0.0f, spread = 0.0f;
   for (int b = threadIdx.x; b < nprep; b += 256) {
     const float* h = hdr + (size_t)(1 + b) * kRecHeader;
@@ -431,6 +451,11 @@ __global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, float* __re
   }
   header_reduce(rmin, rmax, spread, hdr);
   write_bound(a, hdr, esc);
+  if (a.origin != nullptr) {
+    __threadfence();
+    __syncthreads();
+    write_origins(a, rec, hdr, a.origin, oxch);
+  }
 }
 
 // ---- packed helpers --------------------------------------------------------------------------
@@ -522,6 +547,9 @@ template <bool CLAMP, bool FIXED>
 __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, const uint4* __restrict__ At,
                                           const float* __restrict__ Wt, int nrb, uint4* xa, uint4* xb, float* xs,
                                           int lane) {
+  // no fp contraction: the record kernel's origin step (write_origins) runs this code in another
+  // kernel and must reproduce it bit for bit
+#pragma clang fp contract(off)
   {  // the lane's own ray: Sa, Sb and the shift into the exchange
     unsigned x[3], y[3], z[3], P[3];
     split3(p[0], x[0], x[1], x[2]);
@@ -596,6 +624,52 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
   }
   __builtin_amdgcn_wave_barrier();  // the exchange is rewritten by the next step
   return own;
+}
+
+// A march step's soft-min D at p on the matrix cores with the fixed shift sh = rho'_0 (sphere 0;
+// S00 / S10 = its records S0[0] / S1[0]) -- soft_min_march's fixed-shift step, shared with the
+// per-view origin step (write_origins) so that both give the same bits.
+template <bool CLAMP>
+__device__ __forceinline__ float march_d_fixed(const float p[3], float kappa, float inv_kappa, float kr_first,
+                                               const float4& S00, const float4& S10, const uint4* __restrict__ At,
+                                               const float* __restrict__ Wt, int nrb, uint4* xa, uint4* xb,
+                                               float* xs, int lane) {
+#pragma clang fp contract(off)
+  const float k2 = kappa * kappa;
+  const float q0 = fmaf(p[2], S10.x, fmaf(p[1], S00.z, fmaf(p[0], S00.x, fmaf(k2, psq(p), S10.z))));
+  const float sh = fsqrt(fmaxf(q0, k2 * 1e-6f));
+  const float s = lse_mfma<CLAMP, true>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
+  const float m = kr_first - sh;
+  return -(flog2(fmaxf(s, 1e-30f)) + m) * inv_kappa;
+}
+
+// Camera mode: every ray of view v starts its march at the eye (camera.rs:83-85), so the first
+// step's soft-min D(eye) is one number per view. Evaluated here once per view (one wave each) by
+// the march's own code path for that step -- none = false (no previous step), the clamped
+// sweep (no distance bound yet), fixed shift on the matrix cores -- it stands in for the step of
+// every ray bit for bit (rm_ray_kernel). NaN where the first step would take another path
+// (vector-only march, or the fixed shift not provably safe): those rays march it themselves.
+// rec / hdr: this call's complete records and header; xch: kWaves x 64 x 36 B of LDS.
+__device__ void write_origins(const KArgs& a, const float4* rec, const float* hdr, float* orig, unsigned char* xch) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int np = a.Mpad / 2;
+  const float kappa = a.k * kLog2e, inv_kappa = 1.0f / kappa;
+  const float rmax = hdr[1], spread = hdr[2];
+  const bool shift_fixed_ok = kappa * (rmax + spread) * 1.001f <= 100.0f;
+  const float kr_first = kappa * a.radius[0];
+  const uint4* At = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(rec) + tiles_offset(np, (np + 255) / 256));
+  const float* Wt = reinterpret_cast<const float*>(At + (size_t)(np / 8) * 64);
+  uint4* xa = reinterpret_cast<uint4*>(xch) + wave * 64;
+  uint4* xb = reinterpret_cast<uint4*>(xch) + kWaves * 64 + wave * 64;
+  float* xs = reinterpret_cast<float*>(xch) + kWaves * 64 * 8 + wave * 64;
+  for (int v = wave; v < a.num_views; v += kWaves) {
+    const float p[3] = {a.cams[v].eye[0], a.cams[v].eye[1], a.cams[v].eye[2]};
+    float D = __builtin_nanf("");
+    if (a.mfma && shift_fixed_ok && psq(p) <= 1e10f)
+      D = march_d_fixed<true>(p, kappa, inv_kappa, kr_first, rec[4 * np], rec[5 * np], At, Wt, np / 8, xa, xb, xs,
+                              lane);
+    if (lane == 0) orig[v] = D;
+  }
 }
 
 // The march's log-sum-exp in weighted form: rho' = sqrt(k^2 q) = k rho straight from the scaled
@@ -916,10 +990,12 @@ __device__ __forceinline__ void escaped_block(const KArgs& a, const Lds& L, long
 // the launch order (16x16 pixel tiles per block, 8x8 per wave) to the pixel's row of the
 // [N,3] tensors.
 template <bool CAM>
-__device__ __forceinline__ void setup_ray(const KArgs& a, long long& ri, float o[3], float d[3]) {
+__device__ __forceinline__ void setup_ray(const KArgs& a, long long& ri, float o[3], float d[3], int& view) {
+  view = 0;
   if constexpr (CAM) {
     const long long npix = (long long)a.width * a.height;
     const int v = (int)(ri / npix);
+    view = v;
     const long long pix = ri - (long long)v * npix;
     int x, y;
     if (a.tiling == 2) {
@@ -959,7 +1035,8 @@ __global__ __launch_bounds__(kBlock) void rm_escape_kernel(const KArgs a, int* _
   const bool valid = li < a.n_rays;
   long long ri = a.ray_begin + (valid ? li : 0);
   float o[3], d[3];
-  setup_ray<CAM>(a, ri, o, d);
+  int view;
+  setup_ray<CAM>(a, ri, o, d, view);
   float c0[3], R;
   scene_bound(a, scratch, tid, c0, R);
   const bool have_t = MODE == kBwd && a.t_in != nullptr;
@@ -999,7 +1076,8 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
 
   // ray (camera.rs:58-87 in camera mode)
   float o[3], d[3];
-  setup_ray<CAM>(a, ri, o, d);
+  int view;
+  setup_ray<CAM>(a, ri, o, d, view);
 
   // ---- escape skip (RM_MARCH_SKIP_ESCAPED): a block whose rays all provably leave the scene
   // (rm_escape_kernel) gets out = 0 and zero gradients without marching -- exactly what the full
@@ -1046,23 +1124,17 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     const bool fixed = !none && shift_fixed_ok && __all(psq(p) <= 1e10f);
     if ((none || fixed) && a.mfma) {
       const float k2 = kappa * kappa;
-      float sh = 0.0f;
-      if (fixed) {  // the ray's shift: rho'_0 of sphere 0 (any value near it keeps +-100 headroom)
-        const float4 A = Lds::v4(L.S0[0]), B = Lds::v4(L.S1[0]);
-        float q0 = fmaf(p[2], B.x, fmaf(p[1], A.z, fmaf(p[0], A.x, fmaf(k2, psq(p), B.z))));
-        sh = fsqrt(fmaxf(q0, k2 * 1e-6f));
-      }
       const int nrb = a.Mpad / 16;
       uint4* xa = reinterpret_cast<uint4*>(L.slots) + wave * 64;
       uint4* xb = reinterpret_cast<uint4*>(L.slots) + kWaves * 64 + wave * 64;
       float* xs = L.slots + kWaves * 64 * 8 + wave * 64;
-      if (none)
-        s = fast ? lse_mfma<false, false>(p, k2, sh, L.At, L.Wt, nrb, xa, xb, xs, lane)
-                 : lse_mfma<true, false>(p, k2, sh, L.At, L.Wt, nrb, xa, xb, xs, lane);
-      else
-        s = fast ? lse_mfma<false, true>(p, k2, sh, L.At, L.Wt, nrb, xa, xb, xs, lane)
-                 : lse_mfma<true, true>(p, k2, sh, L.At, L.Wt, nrb, xa, xb, xs, lane);
-      if (fixed) m = kr_first - sh;
+      if (fixed) {  // the ray's shift: rho'_0 of sphere 0 (any value near it keeps +-100 headroom)
+        const float4 A = Lds::v4(L.S0[0]), B = Lds::v4(L.S1[0]);
+        return fast ? march_d_fixed<false>(p, kappa, inv_kappa, kr_first, A, B, L.At, L.Wt, nrb, xa, xb, xs, lane)
+                    : march_d_fixed<true>(p, kappa, inv_kappa, kr_first, A, B, L.At, L.Wt, nrb, xa, xb, xs, lane);
+      }
+      s = fast ? lse_mfma<false, false>(p, k2, 0.0f, L.At, L.Wt, nrb, xa, xb, xs, lane)
+               : lse_mfma<true, false>(p, k2, 0.0f, L.At, L.Wt, nrb, xa, xb, xs, lane);
       return -(flog2(fmaxf(s, 1e-30f)) + m) * inv_kappa;
     }
     if (none || fixed) {
@@ -1099,6 +1171,7 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   float lb = -INFINITY;  // lower bound on the scene distance at the current point
   float Dprev = INFINITY;  // previous march step (none yet)
   bool dead = false;       // wave-uniform: every ray of the wave has escaped (see below)
+  int steps_saved = 0;     // wave-uniform: march steps this wave did not run (work statistics)
   // the scene's bounding sphere (c, R) (scene_bound, in the record header); R' = R + soft-min
   // slack + 1e-3 (fp32 margin of the march)
   const float c0x = hdr[4], c0y = hdr[5], c0z = hdr[6];
@@ -1115,34 +1188,57 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     __builtin_amdgcn_s_setprio(3);
     const int half = max(a.steps / 2, 1);
 #endif
-    for (int st = 0; st < a.steps; ++st) {
+    // Escaped rays: receding from the scene's bounding sphere (c_0, R) with every later
+    // soft-min >= |p - c_0| - R - ln(M)/k >= gone_d (the distance only grows along a
+    // receding ray, so t keeps increasing); the reconnected point and the mask argument
+    // are then >= gone_d too, where sigmoid(-msharp D) (or exp(-10 D^2)) is exactly 0 in
+    // fp32: out = 0 and every gradient term is 0, whatever the remaining steps would give.
+    // A wave whose rays have all escaped stops here. Margins: 1e-5 relative + 1e-3 cover
+    // the fp32 rounding of the march at any |p|.
+    // Each remaining step is >= dist - R' long and keeps the ray receding, so the distance
+    // grows step by step (write_bound): with n steps left the ray is gone once
+    // (1 - 1e-5) dist >= T(n) -- proven long before the ray gets there.
+    auto wave_escaped = [&](int st, const float p[3]) {
+      if (!(a.gone_d > 0.0f)) return false;
+      const float ex = p[0] - c0x, ey = p[1] - c0y, ez = p[2] - c0z;
+      const float Tn = esc_tab[min(a.steps - st, kEscTab - 1)];
+      const bool gone = fmaf(ez, d[2], fmaf(ey, d[1], ex * d[0])) >= 0.0f &&
+                        fsqrt(fmaf(ez, ez, fmaf(ey, ey, ex * ex))) * (1.0f - 1e-5f) >= Tn;
+      if (__all(gone || !valid)) {
+        steps_saved += a.steps - st;
+        return true;
+      }
+      return false;
+    };
+    int st0 = 0;
+    if constexpr (CAM) {
+      // Camera mode: step 0 from the soft-min at the eye, evaluated once per view by the same
+      // code path (write_origins), when every lane of the wave has it (not NaN). Taken before
+      // the loop so that D0 holds no register through the march.
+      if (a.origin != nullptr && a.steps > 0) {
+        const float D0 = a.origin[view];
+        if (__all((__float_as_uint(D0) & 0x7fffffffu) <= 0x7f800000u)) {
+          const float p[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
+          if (wave_escaped(0, p)) {
+            dead = true;
+          } else {  // == soft_min_march(p, all_safe(-inf) = false, inf) at p = o = the eye
+            t += D0;
+            lb = D0 - fabsf(D0);
+            Dprev = D0;
+            st0 = 1;
+            steps_saved = 1;  // a step this wave did not run
+          }
+        }
+      }
+    }
+    for (int st = st0; !dead && st < a.steps; ++st) {
 #if RM_PRIO_RAMP
       if (st == half) __builtin_amdgcn_s_setprio(2);
 #endif
       const float p[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
-      if (a.gone_d > 0.0f) {
-        // Escaped rays: receding from the scene's bounding sphere (c_0, R) with every later
-        // soft-min >= |p - c_0| - R - ln(M)/k >= gone_d (the distance only grows along a
-        // receding ray, so t keeps increasing); the reconnected point and the mask argument
-        // are then >= gone_d too, where sigmoid(-msharp D) (or exp(-10 D^2)) is exactly 0 in
-        // fp32: out = 0 and every gradient term is 0, whatever the remaining steps would give.
-        // A wave whose rays have all escaped stops here. Margins: 1e-5 relative + 1e-3 cover
-        // the fp32 rounding of the march at any |p|.
-        // Each remaining step is >= dist - R' long and keeps the ray receding, so the distance
-        // grows step by step (write_bound): with n steps left the ray is gone once
-        // (1 - 1e-5) dist >= T(n) -- proven long before the ray gets there.
-        const float ex = p[0] - c0x, ey = p[1] - c0y, ez = p[2] - c0z;
-        const float Tn = esc_tab[min(a.steps - st, kEscTab - 1)];
-        const bool gone = fmaf(ez, d[2], fmaf(ey, d[1], ex * d[0])) >= 0.0f &&
-                          fsqrt(fmaf(ez, ez, fmaf(ey, ey, ex * ex))) * (1.0f - 1e-5f) >= Tn;
-        if (__all(gone || !valid)) {
-          dead = true;
-          if (a.stats != nullptr && lane == 0) {
-            atomicAdd(a.stats + 1, 1ull);
-            atomicAdd(a.stats + 2, (unsigned long long)(a.steps - st));
-          }
-          break;
-        }
+      if (wave_escaped(st, p)) {
+        dead = true;
+        break;
       }
       const float D = soft_min_march(p, all_safe(lb), Dprev);
       t += D;
@@ -1155,6 +1251,14 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   __builtin_amdgcn_s_setprio(1);
 #endif
   if ((MODE == kFwd || MODE == kRender) && a.t_out != nullptr && valid) a.t_out[ri] = t;
+  // work statistics: per wave here in the forward modes; per block at the hand-off barrier in the
+  // backward modes (one pair of atomics per block, not per wave)
+  if constexpr (MODE == kFwd || MODE == kRender) {
+    if (a.stats != nullptr && lane == 0) {
+      if (dead) atomicAdd(a.stats + 1, 1ull);
+      if (steps_saved != 0) atomicAdd(a.stats + 2, (unsigned long long)steps_saved);
+    }
+  }
 
   // Post-march forward state. A wave whose rays have all escaped (see the march loop) keeps
   // the defaults: out = mix L mu = 0 with mu = 0, and every backward seed is 0.
@@ -1341,15 +1445,29 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   // this barrier such waves end (an ended wave no longer counts in s_barrier) and the others
   // run the backward sweeps and combine only their own partials. The escaped waves' terms are
   // exactly 0, so the record is the one the full computation would write.
-  int* wflag = reinterpret_cast<int*>(L.misc);  // [kWaves]
+  static_assert(2 * kWaves <= 8, "misc layout: flags before the scalars");
+  int* wflag = reinterpret_cast<int*>(L.misc);  // [kWaves] dead flags, [kWaves] steps saved
   float* wscal = L.misc + 8;                     // [kWaves][8]
   {
     const float vals[8] = {gell[0], gell[1], gell[2], gamb, loss, 0.0f, 0.0f, 0.0f};
     const float red = wave_reduce8(vals, lane);
     if ((lane & 7) == 7) wscal[wave * 8 + (lane >> 3)] = red;
-    if (lane == 0) wflag[wave] = dead ? 1 : 0;
+    if (lane == 0) {
+      wflag[wave] = dead ? 1 : 0;
+      wflag[kWaves + wave] = steps_saved;
+    }
   }
   __syncthreads();
+  if (a.stats != nullptr && tid == 0) {
+    int ex = 0, sv = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+      ex += wflag[w];
+      sv += wflag[kWaves + w];
+    }
+    if (ex != 0) atomicAdd(a.stats + 1, (unsigned long long)ex);
+    if (sv != 0) atomicAdd(a.stats + 2, (unsigned long long)sv);
+  }
   int alive = 0;
 #pragma unroll
   for (int w = 0; w < kWaves; ++w) alive |= wflag[w] ? 0 : (1 << w);
@@ -1391,16 +1509,17 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   // (qpair), so dd = dmin - delta <= 0 and v - mA <= 0 hold exactly, as in the lane=ray form.
   {
     (void)slots;
-    float* comb = L.slots;  // [2][kWaves][8][64] per-sphere wave sums (double-buffered)
-    float4* rayd = reinterpret_cast<float4*>(L.slots + 2 * kWaves * 8 * 64) + wave * 64 * 3;
-    float* gpa = L.slots + 2 * kWaves * 8 * 64 + kWaves * 64 * 12 + wave * 64 * 4;
+    constexpr int kComb = RM_BWD_COMB_BUFS * kWaves * 8 * 64;
+    float* comb = L.slots;  // [RM_BWD_COMB_BUFS][kWaves][8][64] per-sphere wave sums
+    float4* rayd = reinterpret_cast<float4*>(L.slots + kComb) + wave * 64 * 3;
+    float* gpa = L.slots + kComb + kWaves * 64 * 12 + wave * 64 * 4;
     const int np = a.Mpad / 2;
     const float4* R4 = reinterpret_cast<const float4*>(a.rec_buf);
     const float2* R2 = reinterpret_cast<const float2*>(R4 + 7 * (size_t)np);
     const int ngrp = (a.Mpad + 63) / 64;
     // the block's live waves sum their per-sphere lane sums in wave order into the record
     auto combine = [&](const float (&v)[8], int ncomp, long long rec_base, int grp) {
-      float* cb = comb + (chunk_ctr & 1) * (kWaves * 8 * 64);
+      float* cb = comb + (RM_BWD_COMB_BUFS > 1 ? (chunk_ctr & 1) * (kWaves * 8 * 64) : 0);
 #pragma unroll
       for (int c = 0; c < 8; ++c)
         if (c < ncomp) cb[(wave * 8 + c) * 64 + lane] = v[c];
@@ -1409,6 +1528,7 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
         const int sl = e / ncomp, c = e - sl * ncomp;
         if (grp * 64 + sl < a.Mpad) rec[rec_base + (long long)(grp * 64 + sl) * ncomp + c] = live_sum(cb + c * 64 + sl, 8 * 64);
       }
+      if (RM_BWD_COMB_BUFS == 1) __syncthreads();  // one buffer: read by every live wave before reuse
       ++chunk_ctr;
     };
     // up to 8 active rays of mask m (lowest first) into idx; returns their count
@@ -2309,12 +2429,17 @@ int run(rm_context* ctx, const Call& c) {
       if (hipMalloc(&ctx->rec, need) != hipSuccess) return fail(ctx, RM_ERR_OOM, "record buffer (%zu B)", need);
       ctx->rec_bytes = need;
     }
+    // camera mode: the per-view first march step at the eye, shared by every ray of the view
+    a.origin = (c.cam && (c.march->flags & RM_MARCH_PER_RAY_ORIGIN) == 0)
+                   ? reinterpret_cast<float*>((char*)ctx->rec + origin_offset(np, nprep))
+                   : nullptr;
     hipLaunchKernelGGL(rm_prep_kernel, dim3(nprep), dim3(256), 0, ctx->stream, a, (float4*)ctx->rec);
     RM_HIP(ctx, hipGetLastError());
     if (nprep > 1) {
       float* hdr = reinterpret_cast<float*>((char*)ctx->rec + (size_t)np * (7 * 16 + 8));
       float* esc = reinterpret_cast<float*>((char*)ctx->rec + esc_offset(np, nprep));
-      hipLaunchKernelGGL(rm_prep_finish, dim3(1), dim3(256), 0, ctx->stream, a, hdr, esc, nprep);
+      hipLaunchKernelGGL(rm_prep_finish, dim3(1), dim3(256), 0, ctx->stream, a, (const float4*)ctx->rec, hdr, esc,
+                         nprep);
       RM_HIP(ctx, hipGetLastError());
     }
     a.rec_buf = (const float4*)ctx->rec;

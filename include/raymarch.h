@@ -97,6 +97,11 @@ typedef struct rm_march {
  * three-part splits of the fp32 operands (equal to the fp32 expansion form to rounding) and
  * the vector units do only sqrt, exp2 and the accumulate. A/B timing. */
 #define RM_MARCH_VALU_ONLY 16
+/* Camera mode: every ray of a view starts at the eye, so by default the first march step's
+ * soft-min D(eye) is evaluated once per view (in the per-call record kernel, by the march's own
+ * code path for that step) and shared by all rays of the view -- bit-identical results, one
+ * march step fewer per ray. This flag makes every ray evaluate it itself. A/B timing. */
+#define RM_MARCH_PER_RAY_ORIGIN 32
 
 /* Pinhole LookAt camera, camera.rs:30-37. Rays are generated in-kernel exactly as
  * create_camera_rays (camera.rs:41-87): rows y then x, u = x/W*2-1, v = -(y/H*2-1). */

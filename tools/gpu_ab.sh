@@ -1,10 +1,12 @@
 #!/bin/bash
 # GPU tests, then bench.py with the defaults and with each extra environment given as an
-# argument (e.g. RM_VALU_ONLY=1); prints value, kernel ms, roofline frac, executed frac.
+# argument (e.g. RM_VALU_ONLY=1, RM_LIB_PATH=burn_raymarching_amd/lib/var/<name>.so); prints
+# value, kernel ms, roofline frac, executed frac, exited-wave share. Every GPU step has its own
+# time limit; a failing step ends the script.
 mkdir -p gpurun_out
-timeout -k 10 700 python -m pytest tests -m gpu -q > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 400 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
 rc=$?
-tail -2 gpurun_out/gpu_tests.log
+tail -3 gpurun_out/gpu_tests.log
 [ $rc -le 1 ] || exit $rc
 i=0
 for e in "" "$@"; do
