@@ -464,6 +464,7 @@ __device__ __forceinline__ f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementw
 __device__ __forceinline__ f2 sqrt2(f2 q) { return f2{fsqrt(q.x), fsqrt(q.y)}; }
 __device__ __forceinline__ f2 exp2v(f2 x) { return f2{fexp2(x.x), fexp2(x.y)}; }
 __device__ __forceinline__ f2 rcp2(f2 x) { return f2{frcp(x.x), frcp(x.y)}; }
+__device__ __forceinline__ f2 rsq2(f2 x) { return f2{frsq(x.x), frsq(x.y)}; }
 __device__ __forceinline__ f2 clamp_q(f2 q) { return f2{fmaxf(q.x, 1e-6f), fmaxf(q.y, 1e-6f)}; }
 __device__ __forceinline__ f2 lo(const float4& v) { return f2{v.x, v.y}; }
 __device__ __forceinline__ f2 hi(const float4& v) { return f2{v.z, v.w}; }
@@ -499,7 +500,7 @@ __device__ __forceinline__ void lse_point(const float p[3], const Lds& L, int np
       const float2 K = L.kr(i0 + ii);
       f2 q = qpair(PX, PY, PZ, PP, A, B);
       if constexpr (CLAMP) q = clamp_q(q);
-      v[ii] = fma2(sqrt2(q), NK, f2{K.x, K.y});
+      v[ii] = fma2(q * rsq2(q), NK, f2{K.x, K.y});  // rho = q rsq(q), as backward sweep 2
     }
     if constexpr (SHIFT != kShiftMax) {
       if constexpr (SHIFT == kShiftFixed) {
@@ -773,81 +774,6 @@ __device__ __forceinline__ void lse_taps_w(const float p[3], const Lds& L, int n
   for (int t = 0; t < 6; ++t) s[t] = acc[t].x + acc[t].y;
 }
 
-// Gradient of the soft-min at p for the detached normal: grad D = sum_j beta_j (p - c_j) / rho_j
-// with beta = softmax(-k dist). scene.rs:81-128 takes central differences of D with eps = 1e-4;
-// this is their eps -> 0 limit (they differ by O(eps^2) times the third derivative of D, ~1e-6
-// relative, below the fp32 noise of the reference's own differences). One sweep instead of six:
-// per sphere one rsq and one exp2. e' = k (p - c) in direct form, q' = |e'|^2,
-// rho' = q' rsq(q') = k rho, and the unnormalised weight 2^(k r) 2^(-rho') (SHIFT none),
-// 2^(k(r - r_0)) 2^(rho'_0 - rho') (fixed) or 2^(k r - rho' - m) with a chunked running max m
-// (max): every shift cancels in sum(w u) / sum(w). Returns grad D in g.
-template <bool CLAMP, int SHIFT>
-__device__ __forceinline__ void grad_sweep(const float p[3], const Lds& L, int npairs, float kappa, float (&g)[3]) {
-  const f2 KPX = sp(kappa * p[0]), KPY = sp(kappa * p[1]), KPZ = sp(kappa * p[2]), HK = sp(0.5f * kappa),
-           QMIN = sp(kappa * kappa * 1e-6f);
-  f2 G[3] = {sp(0.0f), sp(0.0f), sp(0.0f)}, Z = sp(0.0f), SH = sp(0.0f);
-  float m = -INFINITY;
-  for (int i0 = 0; i0 < npairs; i0 += 8) {
-    f2 ex[8], ey[8], ez[8], r[8], arg[8];
-#pragma unroll
-    for (int ii = 0; ii < 8; ++ii) {
-      const float4 A = L.p0(i0 + ii), B = L.p1(i0 + ii);
-      ex[ii] = fma2(HK, lo(A), KPX);
-      ey[ii] = fma2(HK, hi(A), KPY);
-      ez[ii] = fma2(HK, lo(B), KPZ);
-      f2 q = fma2(ez[ii], ez[ii], fma2(ey[ii], ey[ii], ex[ii] * ex[ii]));
-      const f2 qraw = q;
-      if constexpr (CLAMP) q = f2{fmaxf(q.x, QMIN.x), fmaxf(q.y, QMIN.y)};
-      r[ii] = f2{frsq(q.x), frsq(q.y)};
-      const f2 rho = q * r[ii];
-      if constexpr (CLAMP) {  // clamp_min(1e-6): that distance is constant, no gradient
-        r[ii].x = qraw.x >= QMIN.x ? r[ii].x : 0.0f;
-        r[ii].y = qraw.y >= QMIN.y ? r[ii].y : 0.0f;
-      }
-      if constexpr (SHIFT == kShiftFixed) {
-        if (i0 == 0 && ii == 0) SH = sp(rho.x);
-        arg[ii] = SH - rho;
-      } else if constexpr (SHIFT == kShiftNone) {
-        arg[ii] = -rho;
-      } else {
-        const float2 K = L.kr(i0 + ii);
-        arg[ii] = f2{K.x, K.y} - rho;
-      }
-    }
-    f2 MN = sp(0.0f);
-    if constexpr (SHIFT == kShiftMax) {
-      float cm = fmaxf(arg[0].x, arg[0].y);
-#pragma unroll
-      for (int ii = 1; ii < 8; ++ii) cm = fmaxf(cm, fmaxf(arg[ii].x, arg[ii].y));
-      const float mn = fmaxf(m, cm);
-      const f2 sc = sp(fexp2(m - mn));
-      Z *= sc;
-      G[0] *= sc;
-      G[1] *= sc;
-      G[2] *= sc;
-      m = mn;
-      MN = sp(mn);
-    }
-#pragma unroll
-    for (int ii = 0; ii < 8; ++ii) {
-      f2 w = exp2v(SHIFT == kShiftMax ? arg[ii] - MN : arg[ii]);
-      if constexpr (SHIFT != kShiftMax) {
-        const f4v Wt = L.W[i0 + ii];
-        w = w * (SHIFT == kShiftFixed ? f2{Wt.z, Wt.w} : f2{Wt.x, Wt.y});
-      }
-      Z += w;
-      const f2 wr = w * r[ii];
-      G[0] = fma2(wr, ex[ii], G[0]);
-      G[1] = fma2(wr, ey[ii], G[1]);
-      G[2] = fma2(wr, ez[ii], G[2]);
-    }
-  }
-  const float iz = frcp(Z.x + Z.y);
-  g[0] = (G[0].x + G[0].y) * iz;
-  g[1] = (G[1].x + G[1].y) * iz;
-  g[2] = (G[2].x + G[2].y) * iz;
-}
-
 // Distances delta_j = rho_j - r_j at p_final for a pair (shade sweep and backward sweep 1 share it).
 template <bool CLAMP>
 __device__ __forceinline__ f2 delta_pair(const f2& PX, const f2& PY, const f2& PZ, const f2& PP, const float4& A,
@@ -857,6 +783,17 @@ __device__ __forceinline__ f2 delta_pair(const f2& PX, const f2& PY, const f2& P
   if constexpr (CLAMP) q = clamp_q(q);
   rho_out = sqrt2(q);
   return rho_out - hi(R);
+}
+// The same with rho = q rsq(q): one transcendental gives rho and 1/rho (r_out). The differentiable
+// modes' shade sweep and backward sweep 1 both use this form, so their delta agree bit for bit.
+template <bool CLAMP>
+__device__ __forceinline__ f2 delta_pair_rsq(const f2& PX, const f2& PY, const f2& PZ, const f2& PP, const float4& A,
+                                             const float4& B, const float4& R, f2& q_out, f2& r_out) {
+  f2 q = qpair(PX, PY, PZ, PP, A, B);
+  q_out = q;
+  if constexpr (CLAMP) q = clamp_q(q);
+  r_out = rsq2(q);
+  return q * r_out - hi(R);
 }
 
 // Shared sweep at p_final: colour softmax over -csharp*delta (renderer_diff.rs:74-82) and the mask
@@ -900,6 +837,61 @@ __device__ __forceinline__ void shade_sweep(const float p[3], const Lds& L, int 
   }
 }
 
+// The differentiable modes' sweep at p_final: shade_sweep's sums plus the detached normal
+// (scene.rs:81-128, as its eps -> 0 limit f = 2 eps grad D) in the same pass. grad D =
+// sum_j beta_j (p - c_j) / rho_j with beta = softmax(-k delta) -- the mask soft-min's own
+// weights 2^(kappa (dmin - delta_j)) / Zb -- so G accumulates eb (p - c_j) rsq(q_j) next to Zb,
+// rescaled with it when dmin moves (f = 2 eps G / Zb). One rsq per sphere gives rho and 1/rho.
+template <bool CLAMP>
+__device__ __forceinline__ void shade_normal_sweep(const float p[3], const Lds& L, int npairs, float c10l,
+                                                   float kappa, float& dmin, f2& Zw, f2 (&C)[3], f2& Zb,
+                                                   f2 (&G)[3]) {
+  const f2 PX = sp(p[0]), PY = sp(p[1]), PZ = sp(p[2]), PP = sp(psq(p)), CL = sp(c10l), KA = sp(kappa),
+           HALF = sp(0.5f);
+  for (int i0 = 0; i0 < npairs; i0 += 4) {
+    f2 dl[4], r[4];
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      f2 q;
+      dl[ii] = delta_pair_rsq<CLAMP>(PX, PY, PZ, PP, L.p0(i0 + ii), L.p1(i0 + ii), L.p2(i0 + ii), q, r[ii]);
+      if constexpr (CLAMP) {  // clamp_min(1e-6): that distance is constant, no gradient
+        r[ii].x = q.x >= 1e-6f ? r[ii].x : 0.0f;
+        r[ii].y = q.y >= 1e-6f ? r[ii].y : 0.0f;
+      }
+    }
+    float cmin = fminf(dl[0].x, dl[0].y);
+#pragma unroll
+    for (int ii = 1; ii < 4; ++ii) cmin = fminf(cmin, fminf(dl[ii].x, dl[ii].y));
+    const float dn = fminf(dmin, cmin);
+    const f2 sw = sp(fexp2((dn - dmin) * c10l)), sb = sp(fexp2((dn - dmin) * kappa));
+    Zw *= sw;
+    C[0] *= sw;
+    C[1] *= sw;
+    C[2] *= sw;
+    Zb *= sb;
+    G[0] *= sb;
+    G[1] *= sb;
+    G[2] *= sb;
+    dmin = dn;
+    const f2 DN = sp(dn);
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const f2 dd = DN - dl[ii];
+      const f2 ew = exp2v(dd * CL), eb = exp2v(dd * KA);
+      const float4 c3 = L.p3(i0 + ii), A = L.p0(i0 + ii), B = L.p1(i0 + ii);
+      const float2 c4 = L.p4(i0 + ii);
+      Zw += ew;
+      C[0] = fma2(ew, lo(c3), C[0]);
+      C[1] = fma2(ew, hi(c3), C[1]);
+      C[2] = fma2(ew, f2{c4.x, c4.y}, C[2]);
+      Zb += eb;
+      const f2 wr = eb * r[ii];  // p - c = 0.5 (-2c) + p, exactly as the backward's
+      G[0] = fma2(wr, fma2(HALF, lo(A), PX), G[0]);
+      G[1] = fma2(wr, fma2(HALF, hi(A), PY), G[1]);
+      G[2] = fma2(wr, fma2(HALF, lo(B), PZ), G[2]);
+    }
+  }
+}
 
 // ---- the fused per-ray kernel ----------------------------------------------------------
 // Does the ray provably end (after `steps` march steps, or at the given march t) at scene
@@ -1283,30 +1275,21 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
 
     // ---- detached normal (scene.rs:81-128): n = f / sqrt(|f|^2 + 1e-6) with f the central
     // differences (D(p + eps e_a) - D(p - eps e_a))_a; the 1e-6 keeps |n| ~ 0.2 at eps = 1e-4.
+    // ---- colour softmax + mask (renderer_diff.rs:64-90)
+    dmin = INFINITY;
+    f2 Zw2 = sp(0.0f), Zb2 = sp(0.0f), C2[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
     if constexpr (MODE != kRender) {
-      // f = 2 eps grad D (grad_sweep), shift as in the march at p_final: d_min(p_final) <=
-      // d_min(p_a) + |Da| <= 2 max(Da, 0) + ln(M)/k
-      float gD[3];
-      const int np = a.Mpad / 2;
-      const bool none = shift_none_ok && __all(2.0f * fmaxf(Da, 0.0f) + a.lse_slack <= 90.0f * inv_kappa);
-      const bool fixed = !none && shift_fixed_ok && __all(psq(p) <= 1e10f);
-      if (none) {
-        if (fast_f) grad_sweep<false, kShiftNone>(p, L, np, kappa, gD);
-        else grad_sweep<true, kShiftNone>(p, L, np, kappa, gD);
-      } else if (fixed) {
-        if (fast_f) grad_sweep<false, kShiftFixed>(p, L, np, kappa, gD);
-        else grad_sweep<true, kShiftFixed>(p, L, np, kappa, gD);
-      } else {
-        if (fast_f) grad_sweep<false, kShiftMax>(p, L, np, kappa, gD);
-        else grad_sweep<true, kShiftMax>(p, L, np, kappa, gD);
-      }
-      const float te = 2.0f * a.eps;
-      const float nx = te * gD[0], ny = te * gD[1], nz = te * gD[2];
+      // one sweep for both: f = 2 eps grad D (its eps -> 0 limit) with grad D = G / Zb
+      f2 G2[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
+      if (fast_f) shade_normal_sweep<false>(p, L, a.Mpad / 2, c10l, kappa, dmin, Zw2, C2, Zb2, G2);
+      else shade_normal_sweep<true>(p, L, a.Mpad / 2, c10l, kappa, dmin, Zw2, C2, Zb2, G2);
+      const float te = 2.0f * a.eps * frcp(Zb2.x + Zb2.y);
+      const float nx = te * (G2[0].x + G2[0].y), ny = te * (G2[1].x + G2[1].y), nz = te * (G2[2].x + G2[2].y);
       const float inv_len = frsq(fmaf(nz, nz, fmaf(ny, ny, fmaf(nx, nx, 1e-6f))));
       nrm[0] = nx * inv_len;
       nrm[1] = ny * inv_len;
       nrm[2] = nz * inv_len;
-    } else {  // renderer.rs: the six taps themselves
+    } else {  // renderer.rs: the six taps themselves, then the shade sums
       float m6[6], s6[6];
 #pragma unroll
       for (int q = 0; q < 6; ++q) {
@@ -1334,6 +1317,10 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
       nrm[0] = nx * inv_len;
       nrm[1] = ny * inv_len;
       nrm[2] = nz * inv_len;
+      if (fast_f)
+        for_tiles([&](int, int tn) { shade_sweep<false>(p, L, tn / 2, c10l, kappa, dmin, Zw2, C2, Zb2); });
+      else
+        for_tiles([&](int, int tn) { shade_sweep<true>(p, L, tn / 2, c10l, kappa, dmin, Zw2, C2, Zb2); });
     }
 
     // ---- lighting (renderer_diff.rs:48-62; renderer.rs:27-40 in kRender)
@@ -1354,13 +1341,6 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     dif = fmaxf(sdot, 0.0f);
     Lgt = MODE == kRender ? dif + 0.1f : fmaf(dif, 1.0f - amb, amb);
 
-    // ---- colour softmax + mask (renderer_diff.rs:64-90)
-    dmin = INFINITY;
-    f2 Zw2 = sp(0.0f), Zb2 = sp(0.0f), C2[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
-    if (fast_f)
-      for_tiles([&](int, int tn) { shade_sweep<false>(p, L, tn / 2, c10l, kappa, dmin, Zw2, C2, Zb2); });
-    else
-      for_tiles([&](int, int tn) { shade_sweep<true>(p, L, tn / 2, c10l, kappa, dmin, Zw2, C2, Zb2); });
     Zw = Zw2.x + Zw2.y;
     Zb = Zb2.x + Zb2.y;
     Df = dmin - flog2(fmaxf(Zb, 1e-8f)) * inv_kappa;
@@ -1606,9 +1586,8 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
               f2 q = fma2(PZ, GZ, fma2(PY, GY, fma2(PX, GX, PP + CC)));  // == qpair: the shade sweep's q
               const f2 qraw = q;
               if constexpr (CLAMP) q = clamp_q(q);
-              const f2 rho = sqrt2(q);
-              const f2 dl = rho - RR;
-              const f2 ir = rcp2(rho);
+              const f2 ir = rsq2(q);  // == delta_pair_rsq: the shade sweep's delta, and 1/rho
+              const f2 dl = q * ir - RR;
               const f2 dd = DM - dl;  // <= 0 exactly
               const f2 w = exp2v(dd * CL) * IZ;
               const f2 bt = exp2v(dd * KA) * BS;
@@ -1702,9 +1681,9 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
               f2 q = fma2(PZ, GZ, fma2(PY, GY, fma2(PX, GX, PP + CC)));  // == qpair: the reconnect sweep's q
               const f2 qraw = q;
               if constexpr (CLAMP) q = clamp_q(q);
-              const f2 rho = sqrt2(q);
-              const f2 h = exp2v(fma2(rho, NK, KR) - MA) * HS;  // v - mA <= 0 exactly
-              f2 hu = h * rcp2(rho);
+              const f2 r = rsq2(q);  // rho = q rsq(q) as in lse_point, 1/rho = rsq(q)
+              const f2 h = exp2v(fma2(q * r, NK, KR) - MA) * HS;  // v - mA <= 0 exactly
+              f2 hu = h * r;
               if constexpr (CLAMP) {
                 hu.x = qraw.x >= 1e-6f ? hu.x : 0.0f;
                 hu.y = qraw.y >= 1e-6f ? hu.y : 0.0f;
@@ -1743,9 +1722,8 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
             const int i = (jc + jj) / 2 + u;
             const float4 A = L.p0(i), B = L.p1(i), R = L.p2(i), C3 = L.p3(i);
             const float2 C4 = L.p4(i);
-            f2 q, rho;
-            const f2 dl = delta_pair<CLAMP>(PX, PY, PZ, PP, A, B, R, q, rho);  // bitwise the shade sweep's
-            const f2 ir = rcp2(rho);
+            f2 q, ir;
+            const f2 dl = delta_pair_rsq<CLAMP>(PX, PY, PZ, PP, A, B, R, q, ir);  // bitwise the shade sweep's
             const f2 dd = DM - dl;  // <= 0 exactly
             const f2 w = exp2v(dd * CL) * IZ;
             const f2 bt = exp2v(dd * KA) * BS;
@@ -1804,9 +1782,9 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
             f2 q = qpair(PX, PY, PZ, PP, A, B);  // bitwise the reconnect sweep's q
             const f2 qraw = q;
             if constexpr (CLAMP) q = clamp_q(q);
-            const f2 rho = sqrt2(q);
-            const f2 h = exp2v(fma2(rho, NK, f2{K.x, K.y}) - MA) * HS;  // v - mA <= 0 exactly
-            f2 hu = h * rcp2(rho);
+            const f2 r = rsq2(q);  // rho = q rsq(q) as in lse_point, 1/rho = rsq(q)
+            const f2 h = exp2v(fma2(q * r, NK, f2{K.x, K.y}) - MA) * HS;  // v - mA <= 0 exactly
+            f2 hu = h * r;
             if constexpr (CLAMP) {
               hu.x = qraw.x >= 1e-6f ? hu.x : 0.0f;
               hu.y = qraw.y >= 1e-6f ? hu.y : 0.0f;
