@@ -5,11 +5,11 @@ train step at 512x512 / 256 spheres / 32 march steps, on 1..8 MI355X (one proces
 One timed step = one full training step of the reference loop (train.rs:169-198) on the
 HIP path, per rank:
   rm_scene_activate          (scene.rs:41-45)
-  rm_train_step_camera       (4 512x512 views: in-kernel rays, fused forward + compute_loss
+  rm_train_step_camera       (10 512x512 views: in-kernel rays, fused forward + compute_loss
                               seed + analytic backward, fixed-order gradient reduction)
   all_reduce(grads) [N > 1]  (RCCL over xGMI; 7M+4 floats)
   rm_optimizer_step          (activation chain rule + training.rs penalties + Burn Adam)
-Views shard across ranks (weak scaling: every rank renders its own 4 views of 512x512 per step).
+Views shard across ranks (weak scaling: every rank renders its own 10 views of 512x512 per step).
 value = rays of all ranks / max-over-ranks wall time of the K timed steps.
 
 --skip-escaped on (off by default, like the library): ray blocks whose rays provably leave the
@@ -61,10 +61,10 @@ def parse():
     ap.add_argument("--spheres", type=int, default=256)
     ap.add_argument("--march-steps", type=int, default=32)
     ap.add_argument("--smooth-k", type=float, default=32.0)
-    ap.add_argument("--views-per-gpu", type=int, default=4,
-                    help="512x512 views per GPU per step: 4 = 1,048,576 rays = 4096 ray blocks = one launch "
-                         "(4 GPU fills, so the once-per-launch ramp-down and the per-step O(M) kernels are "
-                         "amortised); at 8 GPUs the step covers 32 views")
+    ap.add_argument("--views-per-gpu", type=int, default=10,
+                    help="512x512 views per GPU per step: 10 = the whole 10-camera ring of BASELINE configs[1-2] "
+                         "= 2,621,440 rays = 10240 ray blocks in one launch (the once-per-launch ramp-down and "
+                         "the per-step O(M) kernels are amortised); at 8 GPUs a step covers 80 views")
     ap.add_argument("--ring", type=int, default=10, help="cameras on the target ring")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")

@@ -55,7 +55,7 @@ namespace rm {
 // kRender: the non-differentiable target renderer of renderer.rs:4-80 (generate.rs)
 enum Mode { kFwd = 0, kBwd = 1, kTrain = 2, kRender = 3 };
 
-constexpr int kMaxBlocksPerLaunch = 4096; // bounds the partial-gradient workspace per launch
+constexpr int kMaxBlocksPerLaunch = 16384;  // bounds the partial-gradient workspace per launch (16 views of 512x512)
 constexpr int kReduceSegs = 64;           // block segments of the reduction (<= 256 blocks each)
 
 struct KArgs {
@@ -338,13 +338,17 @@ __device__ void write_bound(const KArgs& a, float* hdr, float* esc) {
 // rm_prep_finish); the final header also gets the scene's bounding sphere (scene_bound).
 constexpr int kPrepStageMax = 512;  // one-block prep: parameters staged in LDS up to this M
 
-__device__ void write_origins(const KArgs& a, const float4* rec, const float* hdr, float* orig, unsigned char* xch);
+__device__ void write_origins(const KArgs& a, const float4* rec, const uint4* At, const float* Wt, const float* hdr,
+                              float* orig, unsigned char* xch);
 
 __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __restrict__ rec) {
   // One-block case: stage the parameters in LDS once (one load round instead of one per phase:
   // records, MFMA tiles, header, bounding sphere); the phases below read them through `a`.
   __shared__ float stage[7 * kPrepStageMax];
   __shared__ __attribute__((aligned(16))) unsigned char oxch[kWaves * 64 * 36];  // write_origins' ray exchange
+  // one-block case: LDS copies of the march tiles for write_origins (no global round trips)
+  __shared__ uint4 sAt[kPrepStageMax / 16 * 64];
+  __shared__ float sWt[kPrepStageMax / 16 * 32];
   KArgs a = a0;
   if (gridDim.x == 1 && a0.M <= kPrepStageMax) {
     const int M = a0.M;
@@ -421,12 +425,18 @@ __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __
   uint4* At = reinterpret_cast<uint4*>(tiles);
   float* Wt = reinterpret_cast<float*>(At + (size_t)nrb * 64);
 #ifndef RM_DBG_NO_TILES
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < nrb * 64; e += gridDim.x * 256) At[e] = mfma_a_frag(a, e >> 6, e & 63);
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < nrb * 64; e += gridDim.x * 256) {
+    const uint4 f = mfma_a_frag(a, e >> 6, e & 63);
+    At[e] = f;
+    if (gridDim.x == 1) sAt[e] = f;
+  }
 #endif
   for (int e = blockIdx.x * 256 + threadIdx.x; e < nrb * 32; e += gridDim.x * 256) {
     const int j = 16 * (e >> 5) + (e & 15);
     const float krj = j < a.M ? kappa * a.radius[j] : 0.0f;
-    Wt[e] = j >= a.M ? 0.0f : ((e & 16) ? fexp2(krj - kr_first) : fexp2(krj));
+    const float w = j >= a.M ? 0.0f : ((e & 16) ? fexp2(krj - kr_first) : fexp2(krj));
+    Wt[e] = w;
+    if (gridDim.x == 1) sWt[e] = w;
   }
   header_reduce(rmin, rmax, spread, gridDim.x == 1 ? hdr : hdr + (size_t)(1 + blockIdx.x) * kRecHeader);
 #ifndef RM_DBG_NO_BOUND
@@ -435,7 +445,7 @@ __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __
   if (gridDim.x == 1 && a.origin != nullptr) {
     __threadfence();
     __syncthreads();  // the records, tiles and header written above are complete and visible
-    write_origins(a, rec, hdr, a.origin, oxch);
+    write_origins(a, rec, sAt, sWt, hdr, a.origin, oxch);
   }
 }
 
@@ -454,7 +464,9 @@ __global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, const float
   if (a.origin != nullptr) {
     __threadfence();
     __syncthreads();
-    write_origins(a, rec, hdr, a.origin, oxch);
+    const int np = a.Mpad / 2;
+    const uint4* At = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(rec) + tiles_offset(np, nprep));
+    write_origins(a, rec, At, reinterpret_cast<const float*>(At + (size_t)(np / 8) * 64), hdr, a.origin, oxch);
   }
 }
 
@@ -650,16 +662,16 @@ __device__ __forceinline__ float march_d_fixed(const float p[3], float kappa, fl
 // sweep (no distance bound yet), fixed shift on the matrix cores -- it stands in for the step of
 // every ray bit for bit (rm_ray_kernel). NaN where the first step would take another path
 // (vector-only march, or the fixed shift not provably safe): those rays march it themselves.
-// rec / hdr: this call's complete records and header; xch: kWaves x 64 x 36 B of LDS.
-__device__ void write_origins(const KArgs& a, const float4* rec, const float* hdr, float* orig, unsigned char* xch) {
+// rec / hdr: this call's complete records and header; At / Wt: its march tiles (global memory or
+// an LDS copy: the same values); xch: kWaves x 64 x 36 B of LDS.
+__device__ void write_origins(const KArgs& a, const float4* rec, const uint4* At, const float* Wt, const float* hdr,
+                              float* orig, unsigned char* xch) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int np = a.Mpad / 2;
   const float kappa = a.k * kLog2e, inv_kappa = 1.0f / kappa;
   const float rmax = hdr[1], spread = hdr[2];
   const bool shift_fixed_ok = kappa * (rmax + spread) * 1.001f <= 100.0f;
   const float kr_first = kappa * a.radius[0];
-  const uint4* At = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(rec) + tiles_offset(np, (np + 255) / 256));
-  const float* Wt = reinterpret_cast<const float*>(At + (size_t)(np / 8) * 64);
   uint4* xa = reinterpret_cast<uint4*>(xch) + wave * 64;
   uint4* xb = reinterpret_cast<uint4*>(xch) + kWaves * 64 + wave * 64;
   float* xs = reinterpret_cast<float*>(xch) + kWaves * 64 * 8 + wave * 64;
@@ -2195,6 +2207,14 @@ int ensure_block_order(rm_context* ctx, int tx, int ty) {
 
 int pad_spheres(int M) { return (M + kSphereAlign - 1) / kSphereAlign * kSphereAlign; }
 
+// Ray blocks per per-ray launch: kMaxBlocksPerLaunch, or less with the environment variable
+// RM_MAX_BLOCKS_PER_LAUNCH (tests use it to exercise the sub-launch split at small sizes).
+long long max_blocks_per_launch() {
+  const char* e = std::getenv("RM_MAX_BLOCKS_PER_LAUNCH");
+  const long long v = e ? std::atoll(e) : 0;
+  return (v >= 1 && v <= kMaxBlocksPerLaunch) ? v : kMaxBlocksPerLaunch;
+}
+
 long long rec_floats(int Mpad) { return (long long)Mpad * 12 + 8; }
 
 size_t ws_need(long long max_rays, int M) {
@@ -2436,7 +2456,7 @@ int run(rm_context* ctx, const Call& c) {
   bool first = true;
   do {
     const long long blocks_left = (n - done + kBlock - 1) / kBlock;
-    const long long nb = std::min<long long>(blocks_left, kMaxBlocksPerLaunch);
+    const long long nb = std::min<long long>(blocks_left, max_blocks_per_launch());
     const long long nr = std::min<long long>(n - done, nb * kBlock);
     a.ray_begin = done;
     a.n_rays = nr;

@@ -26,9 +26,10 @@ def _both(monkeypatch, fn):
 
 
 # (views, W, H): square, non-square (odd tile rows), and 5 x 512^2 = 5120 blocks, which the
-# library splits into a 4-view and a 1-view launch
+# library splits into a 4-view and a 1-view launch (RM_MAX_BLOCKS_PER_LAUNCH = 4096)
 @pytest.mark.parametrize("views,w,h", [(2, 128, 128), (3, 160, 96), (1, 48, 208), (5, 512, 512)])
 def test_train_step_identical_in_any_dispatch_order(mods, monkeypatch, views, w, h):
+    monkeypatch.setenv("RM_MAX_BLOCKS_PER_LAUNCH", "4096")
     torch, model, render = mods
     m, steps = 96, 32
     sc = model.scene_tensors(model.synthetic_scene(m, 5), "cuda")

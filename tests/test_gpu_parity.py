@@ -260,8 +260,10 @@ def test_invalid_arguments_raise(rm):
     assert rc == 1 and b"num_views" in ctx._lib.rm_last_error(ctx.handle)
 
 
-def test_sublaunch_split_large_batch(rm, oracle):
-    """> 4096 blocks (1,048,576 rays) per call: split into sub-launches, gradients accumulated."""
+def test_sublaunch_split_large_batch(rm, oracle, monkeypatch):
+    """More ray blocks than one launch takes (here capped at 4096 blocks = 1,048,576 rays with
+    RM_MAX_BLOCKS_PER_LAUNCH; 16384 by default): split into sub-launches, gradients accumulated."""
+    monkeypatch.setenv("RM_MAX_BLOCKS_PER_LAUNCH", "4096")
     render, model = rm
     sc = model.synthetic_scene(8, 17)
     cams = model.ring_cameras(2)
