@@ -66,6 +66,9 @@ def parse():
                          "= 2,621,440 rays = 10240 ray blocks in one launch (the once-per-launch ramp-down and "
                          "the per-step O(M) kernels are amortised); at 8 GPUs a step covers 80 views")
     ap.add_argument("--ring", type=int, default=10, help="cameras on the target ring")
+    ap.add_argument("--radius-range", type=float, nargs=2, default=None,
+                    help="activated radii U[lo, hi] of the synthetic scenes (default per SURVEY.md 8d: "
+                         "0.03-0.12 up to 256 spheres, 0.02-0.06 up to 1024, 0.01-0.04 beyond)")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-sample", type=int, default=262144, help="rays of the CPU baseline sample")
@@ -105,8 +108,10 @@ def main():
     rays_global = rays_per_rank * world
 
     # ---- synthetic scene, targets, optimizer --------------------------------------------
-    sc0 = rmm.synthetic_scene(M, seed=0)
-    sc1 = rmm.synthetic_scene(M, seed=1)
+    rr = tuple(args.radius_range) if args.radius_range else (
+        (0.03, 0.12) if M <= 256 else ((0.02, 0.06) if M <= 1024 else (0.01, 0.04)))
+    sc0 = rmm.synthetic_scene(M, seed=0, radius_range=rr)
+    sc1 = rmm.synthetic_scene(M, seed=1, radius_range=rr)
     ring = max(args.ring, world * vpg)
     cams = rmm.ring_cameras(ring)
     tgt_scene = rmm.scene_tensors(sc1)
@@ -255,7 +260,8 @@ def main():
             "config": {"workload": f"train step fwd+bwd, {W}x{H} view(s) per GPU, {M} spheres, {S} march steps, "
                                    f"k={K:g}, camera mode, Adam",
                        "width": W, "height": H, "spheres": M, "march_steps": S, "smooth_k": K,
-                       "views_per_gpu": vpg, "rays_per_step": rays_global, "parallelism": f"views-dp{world}"},
+                       "views_per_gpu": vpg, "rays_per_step": rays_global, "radius_range": list(rr),
+                       "parallelism": f"views-dp{world}"},
             "roofline": roofline,
             "cpu_baseline": cpu,
             "escape_skip": {"enabled": args.skip_escaped == "on", "blocks": blocks_run,

@@ -25,6 +25,11 @@ constexpr int kChunkBwd = 32;            // spheres per backward partial-combine
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kSafeRho = 4e-3f;        // rho >= this => max(q, 1e-6) is a no-op (q >= 1.6e-5)
 constexpr float kPadCenter = 1e15f;      // padding sphere center x: distance ~1e15 -> exp() underflows to 0
+// March t is capped here: a ray 1e15 from the scene has mask (and out, and every gradient term)
+// exactly 0, and the cap keeps |p|^2 and the k^2-scaled matrix-core operands finite. (Rays that
+// leave the scene radially double their distance every step: without the cap t overflows to inf
+// after ~120 steps and the fp32 arithmetic turns into NaN; the reference's own march does.)
+constexpr float kTMax = 1e15f;
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 

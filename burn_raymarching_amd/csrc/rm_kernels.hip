@@ -1226,7 +1226,7 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
           if (wave_escaped(0, p)) {
             dead = true;
           } else {  // == soft_min_march(p, all_safe(-inf) = false, inf) at p = o = the eye
-            t += D0;
+            t = fminf(t + D0, kTMax);
             lb = D0 - fabsf(D0);
             Dprev = D0;
             st0 = 1;
@@ -1245,7 +1245,7 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
         break;
       }
       const float D = soft_min_march(p, all_safe(lb), Dprev);
-      t += D;
+      t = fminf(t + D, kTMax);
       // next point: hard min >= soft-min D here, moved by |D|
       lb = D - fabsf(D);
       Dprev = D;
