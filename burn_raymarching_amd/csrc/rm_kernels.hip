@@ -166,7 +166,7 @@ struct Lds {  // the sphere records (global, scalar-loaded) plus the kernel's LD
 // LDS: the backward's two partial buffers, or (during the march) lse_mfma's per-wave ray
 // exchange (64 x (16 + 16 + 4) B per wave); then 256 B of misc scratch.
 // The transposed backward (RM_BWD_TRANSPOSED) uses RM_BWD_COMB_BUFS x kWaves x 8 x 64 combine
-// floats, 64 x 12 ray-data floats and 64 x 4 g_p floats per wave. The LDS of a block decides how
+// floats, 12 x 64 ray-data floats (field-major) and 64 x 4 g_p floats per wave. The LDS of a block decides how
 // many blocks a CU holds once waves leave the march early (their registers free up, the block's
 // LDS stays until its last wave ends): 24.3 KB -> 6 blocks per CU, 32.3 KB -> 4.
 constexpr size_t kSlotBwdT =
@@ -1496,15 +1496,21 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   // position gradient g_p of sweep 1 is a per-ray sum over spheres: it is reduced across the
   // lanes for batches of 8 rays (three transposing reductions) and accumulated in LDS over the
   // sphere groups. Rays whose seeds are zero contribute exact zeros and are skipped (sweep 1:
-  // gm = 0 and b_scale = 0; sweep 2: g_t = 0) -- in practice the escaped rays of live waves.
+  // gm = 0 and b_scale = 0; sweep 2: g_t = 0) -- in practice the escaped rays of live waves:
+  // the others are compacted (rank among the active lanes) into a field-major per-wave LDS
+  // image, so that rays 2i and 2i+1 of the list sit side by side in every field and one
+  // ds_read_b64 per field yields a packed pair (no register moves, wave-uniform addresses). An
+  // odd count is padded with a copy of the last ray whose seeds are zero (exact zero terms).
   // Distances are formed with the same fp32 operations and operands as the forward sweeps
-  // (qpair), so dd = dmin - delta <= 0 and v - mA <= 0 hold exactly, as in the lane=ray form.
+  // (qpair, delta_pair_rsq), so dd = dmin - delta <= 0 and v - mA <= 0 hold exactly, as in the
+  // lane=ray form.
   {
     (void)slots;
     constexpr int kComb = RM_BWD_COMB_BUFS * kWaves * 8 * 64;
-    float* comb = L.slots;  // [RM_BWD_COMB_BUFS][kWaves][8][64] per-sphere wave sums
-    float4* rayd = reinterpret_cast<float4*>(L.slots + kComb) + wave * 64 * 3;
-    float* gpa = L.slots + kComb + kWaves * 64 * 12 + wave * 64 * 4;
+    constexpr int kFields = 12;  // sweep 1: px py pz |p|^2 dmin 1/Zw b_scale mg gm.xyz (11); sweep 2: 6
+    float* comb = L.slots;       // [RM_BWD_COMB_BUFS][kWaves][8][64] per-sphere wave sums
+    float* rayf = L.slots + kComb + wave * 64 * kFields;                  // [field][64 ray slots]
+    float* gpa = L.slots + kComb + kWaves * 64 * kFields + wave * 64 * 4;  // [slot][4] g_p sums
     const int np = a.Mpad / 2;
     const float4* R4 = reinterpret_cast<const float4*>(a.rec_buf);
     const float2* R2 = reinterpret_cast<const float2*>(R4 + 7 * (size_t)np);
@@ -1523,33 +1529,31 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
       if (RM_BWD_COMB_BUFS == 1) __syncthreads();  // one buffer: read by every live wave before reuse
       ++chunk_ctr;
     };
-    // up to 8 active rays of mask m (lowest first) into idx; returns their count
-    auto take8 = [&](unsigned long long& m, int (&idx)[8]) {
-      int nb = 0;
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        if (m != 0ull) {
-          idx[u] = __builtin_ctzll(m);
-          m &= m - 1ull;
-          ++nb;
-        } else {
-          idx[u] = idx[0];
-        }
-      }
-      return nb;
-    };
+    // the packed pair (slots s, s + 1) of field f
+    auto pair = [&](int f, int s) { return *reinterpret_cast<const f2*>(rayf + f * 64 + s); };
+    const unsigned long long below = (1ull << lane) - 1ull;
 
     // ---- sweep 1 at p_final: colour softmax + mask soft-min + p_final(t_final)
-    rayd[lane * 3 + 0] = make_float4(p[0], p[1], p[2], psq(p));
-    rayd[lane * 3 + 1] = make_float4(dmin, invZw, b_scale, mg);
-    rayd[lane * 3 + 2] = make_float4(gm[0], gm[1], gm[2], 0.0f);
-    gpa[lane * 4 + 0] = 0.0f;
-    gpa[lane * 4 + 1] = 0.0f;
-    gpa[lane * 4 + 2] = 0.0f;
     const unsigned long long act1 = __ballot(gm[0] != 0.0f || gm[1] != 0.0f || gm[2] != 0.0f || b_scale != 0.0f);
+    const int n1 = __popcll(act1), rank1 = __popcll(act1 & below);
+    const bool on1 = ((act1 >> lane) & 1ull) != 0ull;
+    if (on1) {
+      const float vals[11] = {p[0], p[1], p[2], psq(p), dmin, invZw, b_scale, mg, gm[0], gm[1], gm[2]};
+#pragma unroll
+      for (int f = 0; f < 11; ++f) rayf[f * 64 + rank1] = vals[f];
+      if ((n1 & 1) && rank1 == n1 - 1) {  // pad: this ray again, zero seeds
+        const float pad[11] = {p[0], p[1], p[2], psq(p), dmin, invZw, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int f = 0; f < 11; ++f) rayf[f * 64 + n1] = pad[f];
+      }
+      gpa[rank1 * 4 + 0] = 0.0f;
+      gpa[rank1 * 4 + 1] = 0.0f;
+      gpa[rank1 * 4 + 2] = 0.0f;
+    }
     __builtin_amdgcn_wave_barrier();
     {
       const f2 CL = sp(c10l), KA = sp(kappa), NCS = sp(-a.csharp);
+      const int npr1 = (n1 + 1) >> 1;
       auto sweep1 = [&](auto clamp_tag) {
         constexpr bool CLAMP = decltype(clamp_tag)::value;
         for (int grp = 0; grp < ngrp; ++grp) {
@@ -1573,28 +1577,19 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
           const f2 GX = sp(gx), GY = sp(gy), GZ = sp(gz), CC = sp(cc), RR = sp(rr), CR = sp(cr), CG = sp(cg),
                    CB = sp(cbl), HX = sp(0.5f * gx), HY = sp(0.5f * gy), HZ = sp(0.5f * gz);
           f2 agc[3] = {sp(0.0f), sp(0.0f), sp(0.0f)}, agr = sp(0.0f), acol[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
-          unsigned long long m = act1;
-          while (m != 0ull) {
-            int idx[8];
-            const int nb = take8(m, idx);
+          for (int b = 0; b < npr1; b += 4) {  // batches of 4 pairs = 8 slots
             float gpv[3][8];
 #pragma unroll
-            for (int u = 0; u < 8; u += 2) {
-              if (u >= nb) {  // batch slots past the last active ray
+            for (int u = 0; u < 4; ++u) {
+              if (b + u >= npr1) {  // batch slots past the last pair
 #pragma unroll
-                for (int c = 0; c < 3; ++c) gpv[c][u] = gpv[c][u + 1] = 0.0f;
+                for (int c = 0; c < 3; ++c) gpv[c][2 * u] = gpv[c][2 * u + 1] = 0.0f;
                 continue;
               }
-              const float4 a0 = rayd[idx[u] * 3], a1 = rayd[idx[u + 1] * 3];
-              const float4 b0 = rayd[idx[u] * 3 + 1], c0 = rayd[idx[u] * 3 + 2];
-              float4 b1 = rayd[idx[u + 1] * 3 + 1], c1 = rayd[idx[u + 1] * 3 + 2];
-              if (u + 1 >= nb) {  // odd count: the second slot repeats a ray with zero seeds (zero terms)
-                b1.y = b1.z = b1.w = 0.0f;
-                c1 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-              }
-              const f2 PX = f2{a0.x, a1.x}, PY = f2{a0.y, a1.y}, PZ = f2{a0.z, a1.z}, PP = f2{a0.w, a1.w};
-              const f2 DM = f2{b0.x, b1.x}, IZ = f2{b0.y, b1.y}, BS = f2{b0.z, b1.z}, MG = f2{b0.w, b1.w};
-              const f2 G0 = f2{c0.x, c1.x}, G1 = f2{c0.y, c1.y}, G2 = f2{c0.z, c1.z};
+              const int s0 = 2 * (b + u);
+              const f2 PX = pair(0, s0), PY = pair(1, s0), PZ = pair(2, s0), PP = pair(3, s0);
+              const f2 DM = pair(4, s0), IZ = pair(5, s0), BS = pair(6, s0), MG = pair(7, s0);
+              const f2 G0 = pair(8, s0), G1 = pair(9, s0), G2 = pair(10, s0);
               f2 q = fma2(PZ, GZ, fma2(PY, GY, fma2(PX, GX, PP + CC)));  // == qpair: the shade sweep's q
               const f2 qraw = q;
               if constexpr (CLAMP) q = clamp_q(q);
@@ -1612,12 +1607,12 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
               }
               const f2 ex = HX + PX, ey = HY + PY, ez = HZ + PZ;  // == fma2(HALF, -2c, p) = p - c
               const f2 px = gu * ex, py = gu * ey, pz = gu * ez;
-              gpv[0][u] = px.x;
-              gpv[0][u + 1] = px.y;
-              gpv[1][u] = py.x;
-              gpv[1][u + 1] = py.y;
-              gpv[2][u] = pz.x;
-              gpv[2][u + 1] = pz.y;
+              gpv[0][2 * u] = px.x;
+              gpv[0][2 * u + 1] = px.y;
+              gpv[1][2 * u] = py.x;
+              gpv[1][2 * u + 1] = py.y;
+              gpv[2][2 * u] = pz.x;
+              gpv[2][2 * u + 1] = pz.y;
               agc[0] -= px;
               agc[1] -= py;
               agc[2] -= pz;
@@ -1627,16 +1622,11 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
               acol[2] = fma2(w, G2, acol[2]);
             }
             const float r0 = wave_reduce8(gpv[0], lane), r1 = wave_reduce8(gpv[1], lane), r2 = wave_reduce8(gpv[2], lane);
-            if ((lane & 7) == 7) {
-              const int k = lane >> 3;
-              int n = idx[0];
-#pragma unroll
-              for (int u = 1; u < 8; ++u) n = k == u ? idx[u] : n;
-              if (k < nb) {
-                gpa[n * 4 + 0] += r0;
-                gpa[n * 4 + 1] += r1;
-                gpa[n * 4 + 2] += r2;
-              }
+            const int slot = 2 * b + (lane >> 3);
+            if ((lane & 7) == 7 && slot < n1) {
+              gpa[slot * 4 + 0] += r0;
+              gpa[slot * 4 + 1] += r1;
+              gpa[slot * 4 + 2] += r2;
             }
           }
           const float v[8] = {agc[0].x + agc[0].y, agc[1].x + agc[1].y, agc[2].x + agc[2].y, agr.x + agr.y,
@@ -1650,15 +1640,26 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
 
     // ---- sweep 2 at p_approx: t_final = t + D(p_approx) -> g_t * softmax(-k dist_a)
     __builtin_amdgcn_wave_barrier();
-    const float gt = fmaf(gpa[lane * 4 + 2], d[2], fmaf(gpa[lane * 4 + 1], d[1], gpa[lane * 4] * d[0]));
+    float gt = 0.0f;
+    if (on1) gt = fmaf(gpa[rank1 * 4 + 2], d[2], fmaf(gpa[rank1 * 4 + 1], d[1], gpa[rank1 * 4] * d[0]));
     const float hs = gt * frcp(sA);
     __syncthreads();  // every wave is done reading the sweep-1 ray data and combine buffers
-    rayd[lane * 3 + 0] = make_float4(pa[0], pa[1], pa[2], psq(pa));
-    rayd[lane * 3 + 1] = make_float4(mA, hs, 0.0f, 0.0f);
     const unsigned long long act2 = __ballot(hs != 0.0f);
+    const int n2 = __popcll(act2), rank2 = __popcll(act2 & below);
+    if (((act2 >> lane) & 1ull) != 0ull) {
+      const float vals[6] = {pa[0], pa[1], pa[2], psq(pa), mA, hs};
+#pragma unroll
+      for (int f = 0; f < 6; ++f) rayf[f * 64 + rank2] = vals[f];
+      if ((n2 & 1) && rank2 == n2 - 1) {  // pad: this ray again, zero seed
+        const float pad[6] = {pa[0], pa[1], pa[2], psq(pa), mA, 0.0f};
+#pragma unroll
+        for (int f = 0; f < 6; ++f) rayf[f * 64 + n2] = pad[f];
+      }
+    }
     __builtin_amdgcn_wave_barrier();
     {
       const f2 NK = sp(nkappa);
+      const int npr2 = (n2 + 1) >> 1;
       auto sweep2 = [&](auto clamp_tag) {
         constexpr bool CLAMP = decltype(clamp_tag)::value;
         for (int grp = 0; grp < ngrp; ++grp) {
@@ -1677,34 +1678,24 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
           const f2 GX = sp(gx), GY = sp(gy), GZ = sp(gz), CC = sp(cc), KR = sp(kr), HX = sp(0.5f * gx),
                    HY = sp(0.5f * gy), HZ = sp(0.5f * gz);
           f2 agc[3] = {sp(0.0f), sp(0.0f), sp(0.0f)}, agr = sp(0.0f);
-          unsigned long long m = act2;
-          while (m != 0ull) {
-            int idx[8];
-            const int nb = take8(m, idx);
-#pragma unroll
-            for (int u = 0; u < 8; u += 2) {
-              if (u >= nb) break;
-              const float4 a0 = rayd[idx[u] * 3], a1 = rayd[idx[u + 1] * 3];
-              const float4 b0 = rayd[idx[u] * 3 + 1];
-              float4 b1 = rayd[idx[u + 1] * 3 + 1];
-              if (u + 1 >= nb) b1.y = 0.0f;
-              const f2 PX = f2{a0.x, a1.x}, PY = f2{a0.y, a1.y}, PZ = f2{a0.z, a1.z}, PP = f2{a0.w, a1.w};
-              const f2 MA = f2{b0.x, b1.x}, HS = f2{b0.y, b1.y};
-              f2 q = fma2(PZ, GZ, fma2(PY, GY, fma2(PX, GX, PP + CC)));  // == qpair: the reconnect sweep's q
-              const f2 qraw = q;
-              if constexpr (CLAMP) q = clamp_q(q);
-              const f2 r = rsq2(q);  // rho = q rsq(q) as in lse_point, 1/rho = rsq(q)
-              const f2 h = exp2v(fma2(q * r, NK, KR) - MA) * HS;  // v - mA <= 0 exactly
-              f2 hu = h * r;
-              if constexpr (CLAMP) {
-                hu.x = qraw.x >= 1e-6f ? hu.x : 0.0f;
-                hu.y = qraw.y >= 1e-6f ? hu.y : 0.0f;
-              }
-              agc[0] = fma2(-hu, HX + PX, agc[0]);
-              agc[1] = fma2(-hu, HY + PY, agc[1]);
-              agc[2] = fma2(-hu, HZ + PZ, agc[2]);
-              agr -= h;
+          for (int i2 = 0; i2 < npr2; ++i2) {
+            const int s0 = 2 * i2;
+            const f2 PX = pair(0, s0), PY = pair(1, s0), PZ = pair(2, s0), PP = pair(3, s0);
+            const f2 MA = pair(4, s0), HS = pair(5, s0);
+            f2 q = fma2(PZ, GZ, fma2(PY, GY, fma2(PX, GX, PP + CC)));  // == qpair: the reconnect sweep's q
+            const f2 qraw = q;
+            if constexpr (CLAMP) q = clamp_q(q);
+            const f2 r = rsq2(q);  // rho = q rsq(q) as in lse_point, 1/rho = rsq(q)
+            const f2 h = exp2v(fma2(q * r, NK, KR) - MA) * HS;  // v - mA <= 0 exactly
+            f2 hu = h * r;
+            if constexpr (CLAMP) {
+              hu.x = qraw.x >= 1e-6f ? hu.x : 0.0f;
+              hu.y = qraw.y >= 1e-6f ? hu.y : 0.0f;
             }
+            agc[0] = fma2(-hu, HX + PX, agc[0]);
+            agc[1] = fma2(-hu, HY + PY, agc[1]);
+            agc[2] = fma2(-hu, HZ + PZ, agc[2]);
+            agr -= h;
           }
           const float v[8] = {agc[0].x + agc[0].y, agc[1].x + agc[1].y, agc[2].x + agc[2].y, agr.x + agr.y,
                               0.0f, 0.0f, 0.0f, 0.0f};

@@ -66,6 +66,8 @@ CASES = [  # (width, spheres, steps, k, seed)
     (64, 8, 40, 5.0, 1),    # reference step count, early-training k
     (48, 64, 32, 32.0, 2),
     (40, 300, 16, 32.0, 3),  # M not a multiple of 32 and > 256
+    (24, 1024, 64, 32.0, 5),  # BASELINE configs[3] sphere and step counts
+    (16, 4096, 128, 32.0, 6),  # configs[4]: 4096 spheres, 128 steps (multi-block record kernel)
 ]
 
 
