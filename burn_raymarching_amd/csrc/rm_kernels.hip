@@ -166,7 +166,7 @@ struct Lds {  // the sphere records (global, scalar-loaded) plus the kernel's LD
 // LDS: the backward's two partial buffers, or (during the march) lse_mfma's per-wave ray
 // exchange (64 x (16 + 16 + 4) B per wave); then 256 B of misc scratch.
 // The transposed backward (RM_BWD_TRANSPOSED) uses RM_BWD_COMB_BUFS x kWaves x 8 x 64 combine
-// floats, 12 x 64 ray-data floats (field-major) and 64 x 4 g_p floats per wave. The LDS of a block decides how
+// floats, 15 x 64 ray-data floats (field-major) and 64 g_t floats per wave. The LDS of a block decides how
 // many blocks a CU holds once waves leave the march early (their registers free up, the block's
 // LDS stays until its last wave ends): 24.3 KB -> 6 blocks per CU, 32.3 KB -> 4.
 constexpr size_t kSlotBwdT =
@@ -1493,9 +1493,10 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   // ---- backward sweeps with one sphere per lane (transposed). The per-sphere gradient sums
   // over the wave's rays accumulate in each lane's registers (no cross-lane reduction); the
   // rays are visited one pair per packed instruction, their data broadcast from LDS. Only the
-  // position gradient g_p of sweep 1 is a per-ray sum over spheres: it is reduced across the
-  // lanes for batches of 8 rays (three transposing reductions) and accumulated in LDS over the
-  // sphere groups. Rays whose seeds are zero contribute exact zeros and are skipped (sweep 1:
+  // position gradient g_p of sweep 1 is a per-ray sum over spheres, and only g_t = g_p . d
+  // (the ray direction) is needed (t_final = t + D(p_a), p = o + d t_final): that scalar is
+  // reduced across the lanes for batches of 8 rays (one transposing reduction) and accumulated
+  // in LDS over the sphere groups. Rays whose seeds are zero contribute exact zeros and are skipped (sweep 1:
   // gm = 0 and b_scale = 0; sweep 2: g_t = 0) -- in practice the escaped rays of live waves:
   // the others are compacted (rank among the active lanes) into a field-major per-wave LDS
   // image, so that rays 2i and 2i+1 of the list sit side by side in every field and one
@@ -1507,10 +1508,10 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   {
     (void)slots;
     constexpr int kComb = RM_BWD_COMB_BUFS * kWaves * 8 * 64;
-    constexpr int kFields = 12;  // sweep 1: px py pz |p|^2 dmin 1/Zw b_scale mg gm.xyz (11); sweep 2: 6
+    constexpr int kFields = 15;  // sweep 1: px py pz |p|^2 dmin 1/Zw b_scale mg gm.xyz d.xyz (14); sweep 2: 6
     float* comb = L.slots;       // [RM_BWD_COMB_BUFS][kWaves][8][64] per-sphere wave sums
-    float* rayf = L.slots + kComb + wave * 64 * kFields;                  // [field][64 ray slots]
-    float* gpa = L.slots + kComb + kWaves * 64 * kFields + wave * 64 * 4;  // [slot][4] g_p sums
+    float* rayf = L.slots + kComb + wave * 64 * kFields;              // [field][64 ray slots]
+    float* gta = L.slots + kComb + kWaves * 64 * kFields + wave * 64;  // [slot] g_t sums
     const int np = a.Mpad / 2;
     const float4* R4 = reinterpret_cast<const float4*>(a.rec_buf);
     const float2* R2 = reinterpret_cast<const float2*>(R4 + 7 * (size_t)np);
@@ -1538,17 +1539,17 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     const int n1 = __popcll(act1), rank1 = __popcll(act1 & below);
     const bool on1 = ((act1 >> lane) & 1ull) != 0ull;
     if (on1) {
-      const float vals[11] = {p[0], p[1], p[2], psq(p), dmin, invZw, b_scale, mg, gm[0], gm[1], gm[2]};
+      const float vals[14] = {p[0], p[1], p[2], psq(p), dmin, invZw, b_scale, mg, gm[0], gm[1], gm[2],
+                              d[0], d[1], d[2]};
 #pragma unroll
-      for (int f = 0; f < 11; ++f) rayf[f * 64 + rank1] = vals[f];
+      for (int f = 0; f < 14; ++f) rayf[f * 64 + rank1] = vals[f];
       if ((n1 & 1) && rank1 == n1 - 1) {  // pad: this ray again, zero seeds
-        const float pad[11] = {p[0], p[1], p[2], psq(p), dmin, invZw, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        const float pad[14] = {p[0], p[1], p[2], psq(p), dmin, invZw, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f,
+                               d[0], d[1], d[2]};
 #pragma unroll
-        for (int f = 0; f < 11; ++f) rayf[f * 64 + n1] = pad[f];
+        for (int f = 0; f < 14; ++f) rayf[f * 64 + n1] = pad[f];
       }
-      gpa[rank1 * 4 + 0] = 0.0f;
-      gpa[rank1 * 4 + 1] = 0.0f;
-      gpa[rank1 * 4 + 2] = 0.0f;
+      gta[rank1] = 0.0f;
     }
     __builtin_amdgcn_wave_barrier();
     {
@@ -1578,18 +1579,18 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
                    CB = sp(cbl), HX = sp(0.5f * gx), HY = sp(0.5f * gy), HZ = sp(0.5f * gz);
           f2 agc[3] = {sp(0.0f), sp(0.0f), sp(0.0f)}, agr = sp(0.0f), acol[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
           for (int b = 0; b < npr1; b += 4) {  // batches of 4 pairs = 8 slots
-            float gpv[3][8];
+            float gtv[8];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
               if (b + u >= npr1) {  // batch slots past the last pair
-#pragma unroll
-                for (int c = 0; c < 3; ++c) gpv[c][2 * u] = gpv[c][2 * u + 1] = 0.0f;
+                gtv[2 * u] = gtv[2 * u + 1] = 0.0f;
                 continue;
               }
               const int s0 = 2 * (b + u);
               const f2 PX = pair(0, s0), PY = pair(1, s0), PZ = pair(2, s0), PP = pair(3, s0);
               const f2 DM = pair(4, s0), IZ = pair(5, s0), BS = pair(6, s0), MG = pair(7, s0);
               const f2 G0 = pair(8, s0), G1 = pair(9, s0), G2 = pair(10, s0);
+              const f2 DX = pair(11, s0), DY = pair(12, s0), DZ = pair(13, s0);
               f2 q = fma2(PZ, GZ, fma2(PY, GY, fma2(PX, GX, PP + CC)));  // == qpair: the shade sweep's q
               const f2 qraw = q;
               if constexpr (CLAMP) q = clamp_q(q);
@@ -1606,28 +1607,21 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
                 gu.y = qraw.y >= 1e-6f ? gu.y : 0.0f;
               }
               const f2 ex = HX + PX, ey = HY + PY, ez = HZ + PZ;  // == fma2(HALF, -2c, p) = p - c
-              const f2 px = gu * ex, py = gu * ey, pz = gu * ez;
-              gpv[0][2 * u] = px.x;
-              gpv[0][2 * u + 1] = px.y;
-              gpv[1][2 * u] = py.x;
-              gpv[1][2 * u + 1] = py.y;
-              gpv[2][2 * u] = pz.x;
-              gpv[2][2 * u + 1] = pz.y;
-              agc[0] -= px;
-              agc[1] -= py;
-              agc[2] -= pz;
+              const f2 ngu = -gu;
+              agc[0] = fma2(ngu, ex, agc[0]);  // gc_j -= g_delta_j u_j
+              agc[1] = fma2(ngu, ey, agc[1]);
+              agc[2] = fma2(ngu, ez, agc[2]);
+              const f2 gt2 = gu * fma2(ez, DZ, fma2(ey, DY, ex * DX));  // (g_delta_j u_j) . d
+              gtv[2 * u] = gt2.x;
+              gtv[2 * u + 1] = gt2.y;
               agr -= gd;
               acol[0] = fma2(w, G0, acol[0]);
               acol[1] = fma2(w, G1, acol[1]);
               acol[2] = fma2(w, G2, acol[2]);
             }
-            const float r0 = wave_reduce8(gpv[0], lane), r1 = wave_reduce8(gpv[1], lane), r2 = wave_reduce8(gpv[2], lane);
+            const float r0 = wave_reduce8(gtv, lane);
             const int slot = 2 * b + (lane >> 3);
-            if ((lane & 7) == 7 && slot < n1) {
-              gpa[slot * 4 + 0] += r0;
-              gpa[slot * 4 + 1] += r1;
-              gpa[slot * 4 + 2] += r2;
-            }
+            if ((lane & 7) == 7 && slot < n1) gta[slot] += r0;
           }
           const float v[8] = {agc[0].x + agc[0].y, agc[1].x + agc[1].y, agc[2].x + agc[2].y, agr.x + agr.y,
                               acol[0].x + acol[0].y, acol[1].x + acol[1].y, acol[2].x + acol[2].y, 0.0f};
@@ -1640,8 +1634,7 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
 
     // ---- sweep 2 at p_approx: t_final = t + D(p_approx) -> g_t * softmax(-k dist_a)
     __builtin_amdgcn_wave_barrier();
-    float gt = 0.0f;
-    if (on1) gt = fmaf(gpa[rank1 * 4 + 2], d[2], fmaf(gpa[rank1 * 4 + 1], d[1], gpa[rank1 * 4] * d[0]));
+    const float gt = on1 ? gta[rank1] : 0.0f;
     const float hs = gt * frcp(sA);
     __syncthreads();  // every wave is done reading the sweep-1 ray data and combine buffers
     const unsigned long long act2 = __ballot(hs != 0.0f);
