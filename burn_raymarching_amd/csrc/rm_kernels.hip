@@ -639,6 +639,25 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
   return own;
 }
 
+// A march step's soft-min D at p on the matrix cores without a shift (soft_min_march's
+// unshifted step; shared with write_origins like march_d_fixed).
+template <bool CLAMP>
+__device__ __forceinline__ float march_d_none(const float p[3], float kappa, float inv_kappa,
+                                              const uint4* __restrict__ At, const float* __restrict__ Wt, int nrb,
+                                              uint4* xa, uint4* xb, float* xs, int lane) {
+#pragma clang fp contract(off)
+  const float s = lse_mfma<CLAMP, false>(p, kappa * kappa, 0.0f, At, Wt, nrb, xa, xb, xs, lane);
+  return -flog2(fmaxf(s, 1e-30f)) * inv_kappa;
+}
+
+// rho'_0 = k |p - c_0| (k = smooth_k log2 e) of sphere 0 from its records S00 / S1[0] = S10: the
+// fixed shift of the march, and (rho'_0 - k r_0 >= k d_min) the unshifted form's admission test.
+__device__ __forceinline__ float fixed_shift(const float p[3], float k2, const float4& S00, const float4& S10) {
+#pragma clang fp contract(off)
+  const float q0 = fmaf(p[2], S10.x, fmaf(p[1], S00.z, fmaf(p[0], S00.x, fmaf(k2, psq(p), S10.z))));
+  return fsqrt(fmaxf(q0, k2 * 1e-6f));
+}
+
 // A march step's soft-min D at p on the matrix cores with the fixed shift sh = rho'_0 (sphere 0;
 // S00 / S10 = its records S0[0] / S1[0]) -- soft_min_march's fixed-shift step, shared with the
 // per-view origin step (write_origins) so that both give the same bits.
@@ -649,8 +668,7 @@ __device__ __forceinline__ float march_d_fixed(const float p[3], float kappa, fl
                                                float* xs, int lane) {
 #pragma clang fp contract(off)
   const float k2 = kappa * kappa;
-  const float q0 = fmaf(p[2], S10.x, fmaf(p[1], S00.z, fmaf(p[0], S00.x, fmaf(k2, psq(p), S10.z))));
-  const float sh = fsqrt(fmaxf(q0, k2 * 1e-6f));
+  const float sh = fixed_shift(p, k2, S00, S10);
   const float s = lse_mfma<CLAMP, true>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
   const float m = kr_first - sh;
   return -(flog2(fmaxf(s, 1e-30f)) + m) * inv_kappa;
@@ -671,6 +689,7 @@ __device__ void write_origins(const KArgs& a, const float4* rec, const uint4* At
   const float kappa = a.k * kLog2e, inv_kappa = 1.0f / kappa;
   const float rmax = hdr[1], spread = hdr[2];
   const bool shift_fixed_ok = kappa * (rmax + spread) * 1.001f <= 100.0f;
+  const bool shift_none_ok = kappa * rmax * 1.001f <= 30.0f;
   const float kr_first = kappa * a.radius[0];
   uint4* xa = reinterpret_cast<uint4*>(xch) + wave * 64;
   uint4* xb = reinterpret_cast<uint4*>(xch) + kWaves * 64 + wave * 64;
@@ -678,7 +697,12 @@ __device__ void write_origins(const KArgs& a, const float4* rec, const uint4* At
   for (int v = wave; v < a.num_views; v += kWaves) {
     const float p[3] = {a.cams[v].eye[0], a.cams[v].eye[1], a.cams[v].eye[2]};
     float D = __builtin_nanf("");
-    if (a.mfma && shift_fixed_ok && psq(p) <= 1e10f)
+    // the first step's choice in soft_min_march: unshifted when sphere 0 proves it safe, else
+    // the fixed shift (else the vector path: not shared)
+    const bool none = a.mfma && shift_none_ok && fixed_shift(p, kappa * kappa, rec[4 * np], rec[5 * np]) - kr_first <= 90.0f;
+    if (none)
+      D = march_d_none<true>(p, kappa, inv_kappa, At, Wt, np / 8, xa, xb, xs, lane);
+    else if (a.mfma && shift_fixed_ok && psq(p) <= 1e10f)
       D = march_d_fixed<true>(p, kappa, inv_kappa, kr_first, rec[4 * np], rec[5 * np], At, Wt, np / 8, xa, xb, xs,
                               lane);
     if (lane == 0) orig[v] = D;
@@ -1123,7 +1147,11 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   // kShiftNone needs the hard maximum -kappa d_min >= -100 at the new point: d_min(new) <=
   // d_min(old) + |D| <= D + ln(M)/k + |D| (the soft-min is within ln(M)/k below the hard min).
   auto soft_min_march = [&](const float p[3], bool fast, float Dprev) {
-    const bool none = shift_none_ok && __all(2.0f * fmaxf(Dprev, 0.0f) + a.lse_slack <= 90.0f * inv_kappa);
+    bool none = shift_none_ok && __all(2.0f * fmaxf(Dprev, 0.0f) + a.lse_slack <= 90.0f * inv_kappa);
+    // or: the nearest sphere is no farther than sphere 0, k (rho_0 - r_0) = rho'_0 - k r_0 <= 90
+    // bounds k d_min just as well (the first steps after the eye, where the 2 D bound is loose)
+    if (!none && shift_none_ok && a.mfma)
+      none = __all(fixed_shift(p, kappa * kappa, Lds::v4(L.S0[0]), Lds::v4(L.S1[0])) - kr_first <= 90.0f);
     float m = none ? 0.0f : -INFINITY, s = 0.0f;
     const bool fixed = !none && shift_fixed_ok && __all(psq(p) <= 1e10f);
     if ((none || fixed) && a.mfma) {
@@ -1137,9 +1165,9 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
         return fast ? march_d_fixed<false>(p, kappa, inv_kappa, kr_first, A, B, L.At, L.Wt, nrb, xa, xb, xs, lane)
                     : march_d_fixed<true>(p, kappa, inv_kappa, kr_first, A, B, L.At, L.Wt, nrb, xa, xb, xs, lane);
       }
-      s = fast ? lse_mfma<false, false>(p, k2, 0.0f, L.At, L.Wt, nrb, xa, xb, xs, lane)
-               : lse_mfma<true, false>(p, k2, 0.0f, L.At, L.Wt, nrb, xa, xb, xs, lane);
-      return -(flog2(fmaxf(s, 1e-30f)) + m) * inv_kappa;
+      (void)k2;
+      return fast ? march_d_none<false>(p, kappa, inv_kappa, L.At, L.Wt, nrb, xa, xb, xs, lane)
+                  : march_d_none<true>(p, kappa, inv_kappa, L.At, L.Wt, nrb, xa, xb, xs, lane);
     }
     if (none || fixed) {
       const float k2 = kappa * kappa;
