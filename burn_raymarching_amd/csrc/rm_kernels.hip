@@ -41,7 +41,10 @@
 #include "rm_device.h"
 
 #ifndef RM_PRIO_RAMP
-#define RM_PRIO_RAMP 1
+// s_setprio ramp over the march / post-march / backward phases: paid off when one launch filled
+// the GPU once (it evened out the co-resident waves' finish); with 10 views per launch and
+// partly-dead blocks backfilled it costs 4 % (1094 vs 1141 Mrays/s), so it is off by default.
+#define RM_PRIO_RAMP 0
 #endif
 #ifndef RM_BWD_TRANSPOSED
 #define RM_BWD_TRANSPOSED 1  // backward sweeps with one sphere per lane (0: one ray per lane)
