@@ -979,8 +979,13 @@ __device__ __forceinline__ long long ray_block(const KArgs& a) {
   // of the scene they see): the XCDs of the dearest view finish last. Rotating the positions
   // inside every full round of 8 blocks by the round number makes each XCD cycle through all
   // views (rank order is kept up to 8 positions, so heavy tiles still start first).
+#ifndef RM_XCD_ROTATE
+#define RM_XCD_ROTATE 1
+#endif
+#if RM_XCD_ROTATE
   const int g = b >> 3;
   if ((g + 1) * 8 <= (int)gridDim.x) b = (g << 3) + (((b & 7) + g) & 7);
+#endif
   const int r = b / a.order_views, v = b - r * a.order_views;
   return (long long)v * a.order_tiles + a.block_order[r];
 }
