@@ -342,16 +342,12 @@ __device__ void write_bound(const KArgs& a, float* hdr, float* esc) {
 constexpr int kPrepStageMax = 512;  // one-block prep: parameters staged in LDS up to this M
 
 __device__ void write_origins(const KArgs& a, const float4* rec, const uint4* At, const float* Wt, const float* hdr,
-                              float* orig, unsigned char* xch);
+                              float* orig, unsigned char* xch, int v);
 
 __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __restrict__ rec) {
   // One-block case: stage the parameters in LDS once (one load round instead of one per phase:
   // records, MFMA tiles, header, bounding sphere); the phases below read them through `a`.
   __shared__ float stage[7 * kPrepStageMax];
-  __shared__ __attribute__((aligned(16))) unsigned char oxch[kWaves * 64 * 36];  // write_origins' ray exchange
-  // one-block case: LDS copies of the march tiles for write_origins (no global round trips)
-  __shared__ uint4 sAt[kPrepStageMax / 16 * 64];
-  __shared__ float sWt[kPrepStageMax / 16 * 32];
   KArgs a = a0;
   if (gridDim.x == 1 && a0.M <= kPrepStageMax) {
     const int M = a0.M;
@@ -428,33 +424,21 @@ __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __
   uint4* At = reinterpret_cast<uint4*>(tiles);
   float* Wt = reinterpret_cast<float*>(At + (size_t)nrb * 64);
 #ifndef RM_DBG_NO_TILES
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < nrb * 64; e += gridDim.x * 256) {
-    const uint4 f = mfma_a_frag(a, e >> 6, e & 63);
-    At[e] = f;
-    if (gridDim.x == 1) sAt[e] = f;
-  }
+  for (int e = blockIdx.x * 256 + threadIdx.x; e < nrb * 64; e += gridDim.x * 256) At[e] = mfma_a_frag(a, e >> 6, e & 63);
 #endif
   for (int e = blockIdx.x * 256 + threadIdx.x; e < nrb * 32; e += gridDim.x * 256) {
     const int j = 16 * (e >> 5) + (e & 15);
     const float krj = j < a.M ? kappa * a.radius[j] : 0.0f;
-    const float w = j >= a.M ? 0.0f : ((e & 16) ? fexp2(krj - kr_first) : fexp2(krj));
-    Wt[e] = w;
-    if (gridDim.x == 1) sWt[e] = w;
+    Wt[e] = j >= a.M ? 0.0f : ((e & 16) ? fexp2(krj - kr_first) : fexp2(krj));
   }
   header_reduce(rmin, rmax, spread, gridDim.x == 1 ? hdr : hdr + (size_t)(1 + blockIdx.x) * kRecHeader);
 #ifndef RM_DBG_NO_BOUND
   if (gridDim.x == 1) write_bound(a, hdr, reinterpret_cast<float*>(reinterpret_cast<char*>(rec) + esc_offset(np, 1)));
 #endif
-  if (gridDim.x == 1 && a.origin != nullptr) {
-    __threadfence();
-    __syncthreads();  // the records, tiles and header written above are complete and visible
-    write_origins(a, rec, sAt, sWt, hdr, a.origin, oxch);
-  }
 }
 
-__global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, const float4* __restrict__ rec,
-                                                      float* __restrict__ hdr, float* __restrict__ esc, int nprep) {
-  __shared__ __attribute__((aligned(16))) unsigned char oxch[kWaves * 64 * 36];
+__global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, float* __restrict__ hdr, float* __restrict__ esc,
+                                                      int nprep) {
   float rmin = INFINITY, rmax = 0.0f, spread = 0.0f;
   for (int b = threadIdx.x; b < nprep; b += 256) {
     const float* h = hdr + (size_t)(1 + b) * kRecHeader;
@@ -464,13 +448,17 @@ __global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, const float
   }
   header_reduce(rmin, rmax, spread, hdr);
   write_bound(a, hdr, esc);
-  if (a.origin != nullptr) {
-    __threadfence();
-    __syncthreads();
-    const int np = a.Mpad / 2;
-    const uint4* At = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(rec) + tiles_offset(np, nprep));
-    write_origins(a, rec, At, reinterpret_cast<const float*>(At + (size_t)(np / 8) * 64), hdr, a.origin, oxch);
-  }
+}
+
+// The per-view origin steps (write_origins), one 64-thread block (one wave) per view, after the
+// records are complete: the views run on separate CUs side by side.
+__global__ __launch_bounds__(64) void rm_origin_kernel(const KArgs a, const float4* __restrict__ rec, int nprep) {
+  __shared__ __attribute__((aligned(16))) unsigned char xch[64 * 36];
+  const int np = a.Mpad / 2;
+  const uint4* At = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(rec) + tiles_offset(np, nprep));
+  const float* Wt = reinterpret_cast<const float*>(At + (size_t)(np / 8) * 64);
+  const float* hdr = reinterpret_cast<const float*>(reinterpret_cast<const float2*>(rec + 7 * (size_t)np) + np);
+  write_origins(a, rec, At, Wt, hdr, a.origin, xch, blockIdx.x);
 }
 
 // ---- packed helpers --------------------------------------------------------------------------
@@ -683,21 +671,21 @@ __device__ __forceinline__ float march_d_fixed(const float p[3], float kappa, fl
 // sweep (no distance bound yet), fixed shift on the matrix cores -- it stands in for the step of
 // every ray bit for bit (rm_ray_kernel). NaN where the first step would take another path
 // (vector-only march, or the fixed shift not provably safe): those rays march it themselves.
-// rec / hdr: this call's complete records and header; At / Wt: its march tiles (global memory or
-// an LDS copy: the same values); xch: kWaves x 64 x 36 B of LDS.
+// rec / hdr: this call's complete records and header; At / Wt: its march tiles; xch: 64 x 36 B
+// of LDS. One wave computes view v.
 __device__ void write_origins(const KArgs& a, const float4* rec, const uint4* At, const float* Wt, const float* hdr,
-                              float* orig, unsigned char* xch) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+                              float* orig, unsigned char* xch, int v) {
+  const int lane = threadIdx.x & 63;
   const int np = a.Mpad / 2;
   const float kappa = a.k * kLog2e, inv_kappa = 1.0f / kappa;
   const float rmax = hdr[1], spread = hdr[2];
   const bool shift_fixed_ok = kappa * (rmax + spread) * 1.001f <= 100.0f;
   const bool shift_none_ok = kappa * rmax * 1.001f <= 30.0f;
   const float kr_first = kappa * a.radius[0];
-  uint4* xa = reinterpret_cast<uint4*>(xch) + wave * 64;
-  uint4* xb = reinterpret_cast<uint4*>(xch) + kWaves * 64 + wave * 64;
-  float* xs = reinterpret_cast<float*>(xch) + kWaves * 64 * 8 + wave * 64;
-  for (int v = wave; v < a.num_views; v += kWaves) {
+  uint4* xa = reinterpret_cast<uint4*>(xch);
+  uint4* xb = reinterpret_cast<uint4*>(xch) + 64;
+  float* xs = reinterpret_cast<float*>(xch) + 64 * 8;
+  {
     const float p[3] = {a.cams[v].eye[0], a.cams[v].eye[1], a.cams[v].eye[2]};
     float D = __builtin_nanf("");
     // the first step's choice in soft_min_march: unshifted when sphere 0 proves it safe, else
@@ -2456,8 +2444,11 @@ int run(rm_context* ctx, const Call& c) {
     if (nprep > 1) {
       float* hdr = reinterpret_cast<float*>((char*)ctx->rec + (size_t)np * (7 * 16 + 8));
       float* esc = reinterpret_cast<float*>((char*)ctx->rec + esc_offset(np, nprep));
-      hipLaunchKernelGGL(rm_prep_finish, dim3(1), dim3(256), 0, ctx->stream, a, (const float4*)ctx->rec, hdr, esc,
-                         nprep);
+      hipLaunchKernelGGL(rm_prep_finish, dim3(1), dim3(256), 0, ctx->stream, a, hdr, esc, nprep);
+      RM_HIP(ctx, hipGetLastError());
+    }
+    if (a.origin != nullptr) {
+      hipLaunchKernelGGL(rm_origin_kernel, dim3(c.views), dim3(64), 0, ctx->stream, a, (const float4*)ctx->rec, nprep);
       RM_HIP(ctx, hipGetLastError());
     }
     a.rec_buf = (const float4*)ctx->rec;
