@@ -42,6 +42,16 @@ def test_python_binding_covers_header(native):
     assert sorted(native.SIGNATURES) == header_functions()
 
 
+def test_header_constants_match_binding(native):
+    """Every #define of include/raymarch.h that the Python binding mirrors has the same value."""
+    text = open(HEADER).read()
+    defines = dict(re.findall(r"#define\s+(RM_[A-Z0-9_]+)\s+(-?\d+)", text))
+    mirrored = [k for k in defines if hasattr(native, k)]
+    assert {"RM_MARCH_SKIP_ESCAPED", "RM_MARCH_PER_RAY_ORIGIN", "RM_MAX_VIEWS_PER_CALL"} <= set(mirrored)
+    for k in mirrored:
+        assert getattr(native, k) == int(defines[k]), k
+
+
 def test_version_and_defaults(native):
     lib = native.lib()
     assert b"gfx950" in lib.rm_version()
