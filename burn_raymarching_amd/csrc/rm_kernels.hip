@@ -49,6 +49,14 @@
 #ifndef RM_BWD_TRANSPOSED
 #define RM_BWD_TRANSPOSED 1  // backward sweeps with one sphere per lane (0: one ray per lane)
 #endif
+#ifndef RM_MARCH_SCHED
+#define RM_MARCH_SCHED 1  // scheduling barriers in the matrix-core march loop (0: compiler's order)
+#endif
+#if RM_MARCH_SCHED
+#define RM_SCHED_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define RM_SCHED_BARRIER() ((void)0)
+#endif
 #ifndef RM_BWD_COMB_BUFS
 #define RM_BWD_COMB_BUFS 1  // transposed backward: combine buffers (1 keeps the block's LDS <= 32 KB)
 #endif
@@ -606,16 +614,16 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
     tile(A, D);
     const bf16x8 A1 = load_a(rb + 1);
     const float4 w1 = load_w(rb + 1);
-    __builtin_amdgcn_sched_barrier(0);  // keep the loads a tile ahead of their use
+    RM_SCHED_BARRIER();  // keep the loads a tile ahead of their use
     consume(D, w);
-    __builtin_amdgcn_sched_barrier(0);
+    RM_SCHED_BARRIER();
     tile(A1, D);
     const int rn = min(rb + 2, nrb - 1);
     A = load_a(rn);
     w = load_w(rn);
-    __builtin_amdgcn_sched_barrier(0);
+    RM_SCHED_BARRIER();
     consume(D, w1);
-    __builtin_amdgcn_sched_barrier(0);
+    RM_SCHED_BARRIER();
   }
   // partial sums of ray 16cb + n sit in the four lane groups: reduce across them, keep own ray
   float own = 0.0f;
