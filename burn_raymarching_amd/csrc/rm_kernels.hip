@@ -67,7 +67,10 @@ namespace rm {
 enum Mode { kFwd = 0, kBwd = 1, kTrain = 2, kRender = 3 };
 
 constexpr int kMaxBlocksPerLaunch = 16384;  // bounds the partial-gradient workspace per launch (16 views of 512x512)
-constexpr int kReduceSegs = 64;           // block segments of the reduction (<= 256 blocks each)
+#ifndef RM_REDUCE_SEGS
+#define RM_REDUCE_SEGS 64
+#endif
+constexpr int kReduceSegs = RM_REDUCE_SEGS;  // block segments of the reduction
 
 struct KArgs {
   // rays: array mode (org/dir) or camera mode (cams)
