@@ -89,6 +89,7 @@ struct KArgs {
   const int* esc_flags;       // nullable: per-block escape flags of this launch (rm_escape_kernel)
   const int* block_order;     // nullable: heavy-first dispatch order of the tiles of a view (ray_block)
   int order_views, order_tiles;
+  const int* cost_order;      // nullable: launch position -> block, by the previous launch's cost (rm_order_kernel)
   CamBasis cams[RM_MAX_VIEWS_PER_CALL];
   // activated scene
   const float* centers;
@@ -985,6 +986,7 @@ __device__ __forceinline__ long long ray_block(const KArgs& a) {
   const int g = b >> 3;
   if ((g + 1) * 8 <= (int)gridDim.x) b = (g << 3) + (((b & 7) + g) & 7);
 #endif
+  if (a.cost_order != nullptr) return a.cost_order[b];
   const int r = b / a.order_views, v = b - r * a.order_views;
   return (long long)v * a.order_tiles + a.block_order[r];
 }
@@ -1851,7 +1853,7 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     float acc = wscal[lane];
 #pragma unroll
     for (int w = 1; w < kWaves; ++w) acc += wscal[w * 8 + lane];
-    rec[(long long)a.Mpad * 12 + lane] = lane == 7 ? 1.0f : acc;  // scalar 7: live flag
+    rec[(long long)a.Mpad * 12 + lane] = lane == 7 ? (float)__popc(alive) : acc;  // scalar 7: live waves (> 0: live)
   }
 }
 
@@ -2149,6 +2151,67 @@ __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restri
   }
 }
 
+// Dispatch order by cost: the previous launch over the same views left each block's number of
+// live waves (0-4: how many waves marched to the end and ran the backward) in scalar 7 of its
+// partial record. Blocks of equal cost are dispatched together -- heaviest first, centre-out
+// within a class -- so co-resident blocks finish together (mixing heavy and light blocks costs
+// 9 %, tools/gpu_ab_rep.sh). One block of 1024 threads: a stable counting sort of the
+// centre-out positions by class. Only the dispatch order changes: results are identical.
+__global__ __launch_bounds__(1024) void rm_order_kernel(const float* __restrict__ P, long long rec, int Mpad, int nb,
+                                                        const int* __restrict__ block_order, int views, int tiles,
+                                                        int* __restrict__ out) {
+  constexpr int kCls = 5;
+  __shared__ int wsum[kCls][16];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int chunk = (nb + 1023) / 1024;
+  const int p0 = min(tid * chunk, nb), p1 = min(p0 + chunk, nb);
+  auto logical = [&](int p) {
+    const int r = p / views, v = p - r * views;
+    return v * tiles + block_order[r];
+  };
+  auto cls = [&](int blk) {
+    const int live = (int)P[(long long)blk * rec + (long long)Mpad * 12 + 7];
+    return kCls - 1 - min(max(live, 0), kCls - 1);  // 0: four live waves ... 4: none
+  };
+  int cnt[kCls] = {0, 0, 0, 0, 0};
+  for (int p = p0; p < p1; ++p) ++cnt[cls(logical(p))];
+  // exclusive scan of the per-thread counts of every class over the block, in thread order
+  int pre[kCls];
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) {
+    int x = cnt[c];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    pre[c] = x - cnt[c];
+    if (lane == 63) wsum[c][wave] = x;
+  }
+  __syncthreads();
+  int base[kCls], total = 0;
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) {
+    int before = 0, all = 0;
+    for (int w = 0; w < 16; ++w) {
+      before += w < wave ? wsum[c][w] : 0;
+      all += wsum[c][w];
+    }
+    base[c] = total + before + pre[c];
+    total += all;
+  }
+  for (int p = p0; p < p1; ++p) {
+    const int blk = logical(p);
+    const int c = cls(blk);
+    int pos = base[0];
+#pragma unroll
+    for (int k = 1; k < kCls; ++k) pos = c == k ? base[k] : pos;
+    out[pos] = blk;
+#pragma unroll
+    for (int k = 0; k < kCls; ++k) base[k] += c == k ? 1 : 0;
+  }
+}
+
 __global__ void rm_sum_small(const float* __restrict__ parts, int n, float* __restrict__ out) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     float acc = 0.0f;
@@ -2178,6 +2241,9 @@ struct rm_context {
   long long stats_blocks = 0;               // ray blocks launched while stats are on
   int* block_order = nullptr;               // centre-out tile order for order_tx x order_ty tiles
   int order_tx = 0, order_ty = 0;
+  int* cost_order = nullptr;                // launch position -> block by the previous launch's cost
+  unsigned long long cost_key = 0;          // geometry of the launch whose partials the workspace holds
+  bool cost_valid = false;
 };
 
 namespace {
@@ -2212,6 +2278,19 @@ int ensure_block_order(rm_context* ctx, int tx, int ty) {
     return dx * dx + dy * dy;
   };
   std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return key(x) < key(y); });
+  if (const char* e = std::getenv("RM_ORDER_EXPERIMENT")) {  // A/B of dispatch orders (timing only)
+    const int mode = std::atoi(e);
+    if (mode == 1) std::reverse(ord.begin(), ord.end());  // border tiles first
+    if (mode == 2) {  // alternate centre and border: heavy and light blocks interleaved
+      std::vector<int> o2;
+      size_t lo = 0, hi = ord.size();
+      while (lo < hi) {
+        o2.push_back(ord[lo++]);
+        if (lo < hi) o2.push_back(ord[--hi]);
+      }
+      ord.swap(o2);
+    }
+  }
   if (ctx->block_order) {
     RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
     RM_HIP(ctx, hipFree(ctx->block_order));
@@ -2487,6 +2566,7 @@ int run(rm_context* ctx, const Call& c) {
     if (ctx->stats_dev) ctx->stats_blocks += nb;
     a.esc_flags = nullptr;
     a.block_order = nullptr;
+    a.cost_order = nullptr;
     const long long npix = (long long)c.W * c.H;
     if (c.cam && a.tiling == 2 && nb > 1 && done % npix == 0 && nr % npix == 0 && nr == nb * kBlock &&
         (c.march->flags & RM_MARCH_NATURAL_ORDER) == 0) {
@@ -2494,6 +2574,25 @@ int run(rm_context* ctx, const Call& c) {
       a.block_order = ctx->block_order;
       a.order_views = (int)(nr / npix);
       a.order_tiles = (int)(npix / kBlock);
+    }
+    // cost-ordered dispatch from the previous launch over the same views (single-launch calls)
+    const bool has_rec = c.mode == kBwd || c.mode == kTrain;
+    unsigned long long key = 0;
+    if (a.block_order != nullptr && has_rec && nb == blocks_left && done == 0 &&
+        (c.march->flags & RM_MARCH_STATIC_ORDER) == 0) {
+      key = ((unsigned long long)c.W << 48) ^ ((unsigned long long)c.H << 32) ^ ((unsigned long long)c.views << 24) ^
+            ((unsigned long long)Mpad << 1) ^ 1ull;
+      if (ctx->cost_valid && ctx->cost_key == key) {
+        if (!ctx->cost_order) RM_HIP(ctx, hipMalloc(&ctx->cost_order, sizeof(int) * kMaxBlocksPerLaunch));
+        hipLaunchKernelGGL(rm_order_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const float*)P, a.rec, Mpad,
+                           (int)nb, (const int*)ctx->block_order, a.order_views, a.order_tiles, ctx->cost_order);
+        RM_HIP(ctx, hipGetLastError());
+        a.cost_order = ctx->cost_order;
+      }
+    }
+    if (has_rec) {  // this launch's partials replace the workspace's
+      ctx->cost_valid = key != 0;
+      ctx->cost_key = key;
     }
     if (nb > 0 && a.cull) {
       if (!ctx->esc_flags) RM_HIP(ctx, hipMalloc(&ctx->esc_flags, sizeof(int) * kMaxBlocksPerLaunch));
@@ -2641,11 +2740,12 @@ int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset) {
 
 void rm_destroy(rm_context* ctx) {
   if (!ctx) return;
-  if (ctx->stats_dev || ctx->esc_flags || ctx->rec || ctx->block_order) {
+  if (ctx->stats_dev || ctx->esc_flags || ctx->rec || ctx->block_order || ctx->cost_order) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stats_dev) (void)hipFree(ctx->stats_dev);
     if (ctx->esc_flags) (void)hipFree(ctx->esc_flags);
     if (ctx->block_order) (void)hipFree(ctx->block_order);
+    if (ctx->cost_order) (void)hipFree(ctx->cost_order);
     if (ctx->rec) (void)hipFree(ctx->rec);
   }
   for (auto& pr : ctx->events) {

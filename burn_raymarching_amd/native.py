@@ -39,6 +39,7 @@ RM_MARCH_NO_EARLY_EXIT = 4
 RM_MARCH_NATURAL_ORDER = 8
 RM_MARCH_VALU_ONLY = 16
 RM_MARCH_PER_RAY_ORIGIN = 32
+RM_MARCH_STATIC_ORDER = 64
 
 
 class RmStats(ctypes.Structure):
@@ -184,7 +185,7 @@ def march_params(steps=40, smooth_k=32.0, normal_eps=1e-4, color_sharpness=10.0,
     env RM_ROW_ORDER=1 adds RM_MARCH_ROW_ORDER (camera-mode row order instead of 16x16 tiles),
     env RM_NO_EARLY_EXIT=1 adds RM_MARCH_NO_EARLY_EXIT, env RM_NATURAL_ORDER=1 adds
     RM_MARCH_NATURAL_ORDER, env RM_VALU_ONLY=1 adds RM_MARCH_VALU_ONLY, env RM_PER_RAY_ORIGIN=1 adds
-    RM_MARCH_PER_RAY_ORIGIN (A/B tests)."""
+    RM_MARCH_PER_RAY_ORIGIN, env RM_STATIC_ORDER=1 adds RM_MARCH_STATIC_ORDER (A/B tests)."""
     if skip_escaped is None:
         skip_escaped = os.environ.get("RM_SKIP_ESCAPED", "0") == "1"
     flags = (RM_MARCH_SKIP_ESCAPED if skip_escaped else 0) | (RM_MARCH_ROW_ORDER if os.environ.get("RM_ROW_ORDER") == "1"
@@ -197,6 +198,8 @@ def march_params(steps=40, smooth_k=32.0, normal_eps=1e-4, color_sharpness=10.0,
         flags |= RM_MARCH_VALU_ONLY
     if os.environ.get("RM_PER_RAY_ORIGIN") == "1":
         flags |= RM_MARCH_PER_RAY_ORIGIN
+    if os.environ.get("RM_STATIC_ORDER") == "1":
+        flags |= RM_MARCH_STATIC_ORDER
     return RmMarch(int(steps), float(smooth_k), float(normal_eps), float(color_sharpness), float(mask_sharpness),
                    flags)
 

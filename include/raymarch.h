@@ -102,6 +102,11 @@ typedef struct rm_march {
  * code path for that step) and shared by all rays of the view -- bit-identical results, one
  * march step fewer per ray. This flag makes every ray evaluate it itself. A/B timing. */
 #define RM_MARCH_PER_RAY_ORIGIN 32
+/* Train / backward calls over the same views (one launch): by default the ray blocks are
+ * dispatched grouped by the cost they had in the previous such call (its number of live
+ * waves), heaviest first; this flag keeps the static centre-out order. Results are identical
+ * either way. A/B timing. */
+#define RM_MARCH_STATIC_ORDER 64
 
 /* Pinhole LookAt camera, camera.rs:30-37. Rays are generated in-kernel exactly as
  * create_camera_rays (camera.rs:41-87): rows y then x, u = x/W*2-1, v = -(y/H*2-1). */

@@ -59,3 +59,38 @@ def test_forward_and_backward_identical_in_any_dispatch_order(mods, monkeypatch)
     b0, b1 = _both(monkeypatch, lambda: render.render_diff_backward_camera(cams, 96, 64, sc, 32.0, g, 32))
     for key in b0:
         assert torch.equal(b0[key], b1[key]), key
+
+
+def test_cost_ordered_dispatch_identical(mods, monkeypatch):
+    """Cost-ordered dispatch (default for repeated train/backward calls over the same views; the
+    order comes from the previous call's live waves per block, RM_MARCH_STATIC_ORDER / env
+    RM_STATIC_ORDER=1 turns it off): the second call of a pair uses it, and its images, loss and
+    gradients equal (==) the static centre-out order's."""
+    torch, model, render = mods
+    sc = model.scene_tensors(model.synthetic_scene(96, 8), "cuda")
+    cams = model.ring_cameras(10)[1:5]
+    tgt = render.render_diff_camera(cams, 128, 128, model.scene_tensors(model.synthetic_scene(96, 9), "cuda"), 32.0, 32)
+
+    def run():
+        out = torch.empty_like(tgt)
+        loss, g, _ = render.train_step_camera(cams, 128, 128, tgt, sc, 32.0, 0.5, 32, out=out)
+        torch.cuda.synchronize()
+        return loss.clone(), {key: v.clone() for key, v in g.items()}, out
+
+    monkeypatch.setenv("RM_STATIC_ORDER", "1")
+    l0, g0, o0 = run()
+    monkeypatch.setenv("RM_STATIC_ORDER", "0")
+    run()                  # establishes the cost history
+    l1, g1, o1 = run()     # dispatched by cost
+    assert torch.equal(o0, o1)
+    assert torch.equal(l0, l1)
+    for key in g0:
+        assert torch.equal(g0[key], g1[key]), key
+    g = torch.randn((4 * 128 * 128, 3), device="cuda", generator=torch.Generator("cuda").manual_seed(3))
+    monkeypatch.setenv("RM_STATIC_ORDER", "1")
+    b0 = render.render_diff_backward_camera(cams, 128, 128, sc, 32.0, g, 32)
+    monkeypatch.setenv("RM_STATIC_ORDER", "0")
+    render.render_diff_backward_camera(cams, 128, 128, sc, 32.0, g, 32)
+    b1 = render.render_diff_backward_camera(cams, 128, 128, sc, 32.0, g, 32)
+    for key in b0:
+        assert torch.equal(b0[key], b1[key]), key
