@@ -30,6 +30,9 @@ constexpr float kPadCenter = 1e15f;      // padding sphere center x: distance ~1
 // leave the scene radially double their distance every step: without the cap t overflows to inf
 // after ~120 steps and the fp32 arithmetic turns into NaN; the reference's own march does.)
 constexpr float kTMax = 1e15f;
+// A live wave's post-march forward and backward sweeps in march-step units (the cost-ordered
+// dispatch's estimate; tools/bench_parts.py: ~8-10).
+constexpr int kPostCost = 10;
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 

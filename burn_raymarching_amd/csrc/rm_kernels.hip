@@ -57,6 +57,9 @@
 #else
 #define RM_SCHED_BARRIER() ((void)0)
 #endif
+#ifndef RM_ORDER_CLASSES
+#define RM_ORDER_CLASSES 16  // cost classes of the cost-ordered dispatch (rm_order_kernel)
+#endif
 #ifndef RM_BWD_COMB_BUFS
 #define RM_BWD_COMB_BUFS 1  // transposed backward: combine buffers (1 keeps the block's LDS <= 32 KB)
 #endif
@@ -1478,7 +1481,10 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   int* wflag = reinterpret_cast<int*>(L.misc);  // [kWaves] dead flags, [kWaves] steps saved
   float* wscal = L.misc + 8;                     // [kWaves][8]
   {
-    const float vals[8] = {gell[0], gell[1], gell[2], gamb, loss, 0.0f, 0.0f, 0.0f};
+    // scalar 6: the wave's cost in march-step units (steps it ran, + kPostCost if it ran the
+    // post-march forward and the backward), for the next call's cost-ordered dispatch
+    const float cost = lane == 0 ? (float)(a.steps - steps_saved + (dead ? 0 : kPostCost)) : 0.0f;
+    const float vals[8] = {gell[0], gell[1], gell[2], gamb, loss, 0.0f, cost, 0.0f};
     const float red = wave_reduce8(vals, lane);
     if ((lane & 7) == 7) wscal[wave * 8 + (lane >> 3)] = red;
     if (lane == 0) {
@@ -1853,7 +1859,7 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     float acc = wscal[lane];
 #pragma unroll
     for (int w = 1; w < kWaves; ++w) acc += wscal[w * 8 + lane];
-    rec[(long long)a.Mpad * 12 + lane] = lane == 7 ? (float)__popc(alive) : acc;  // scalar 7: live waves (> 0: live)
+    rec[(long long)a.Mpad * 12 + lane] = lane == 7 ? 1.0f : acc;  // scalar 7: live flag
   }
 }
 
@@ -2151,17 +2157,19 @@ __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restri
   }
 }
 
-// Dispatch order by cost: the previous launch over the same views left each block's number of
-// live waves (0-4: how many waves marched to the end and ran the backward) in scalar 7 of its
-// partial record. Blocks of equal cost are dispatched together -- heaviest first, centre-out
-// within a class -- so co-resident blocks finish together (mixing heavy and light blocks costs
-// 9 %, tools/gpu_ab_rep.sh). One block of 1024 threads: a stable counting sort of the
-// centre-out positions by class. Only the dispatch order changes: results are identical.
+// Dispatch order by cost: the previous launch over the same views left each block's cost (march
+// steps its waves ran + kPostCost per wave that ran the post-march forward and the backward) in
+// scalar 6 of its partial record. Blocks of similar cost (RM_ORDER_CLASSES classes) are
+// dispatched together -- dearest first, centre-out within a class -- so co-resident blocks
+// finish together (mixing heavy and light blocks costs 9 %, tools/gpu_ab_rep.sh). One block of
+// 1024 threads: a stable counting sort of the centre-out positions by class. Only the dispatch
+// order changes: results are identical.
 __global__ __launch_bounds__(1024) void rm_order_kernel(const float* __restrict__ P, long long rec, int Mpad, int nb,
                                                         const int* __restrict__ block_order, int views, int tiles,
-                                                        int* __restrict__ out) {
-  constexpr int kCls = 5;
+                                                        int steps, int* __restrict__ out) {
+  constexpr int kCls = RM_ORDER_CLASSES;
   __shared__ int wsum[kCls][16];
+  const float cls_scale = (float)kCls / (float)(kWaves * (steps + kPostCost) + 1);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int chunk = (nb + 1023) / 1024;
   const int p0 = min(tid * chunk, nb), p1 = min(p0 + chunk, nb);
@@ -2169,11 +2177,14 @@ __global__ __launch_bounds__(1024) void rm_order_kernel(const float* __restrict_
     const int r = p / views, v = p - r * views;
     return v * tiles + block_order[r];
   };
-  auto cls = [&](int blk) {
-    const int live = (int)P[(long long)blk * rec + (long long)Mpad * 12 + 7];
-    return kCls - 1 - min(max(live, 0), kCls - 1);  // 0: four live waves ... 4: none
+  auto cls = [&](int blk) {  // 0: the dearest blocks
+    const float cost = P[(long long)blk * rec + (long long)Mpad * 12 + 6];
+    const int c = (int)(fminf(fmaxf(cost, 0.0f) * cls_scale, (float)(kCls - 1)));
+    return kCls - 1 - c;
   };
-  int cnt[kCls] = {0, 0, 0, 0, 0};
+  int cnt[kCls];
+#pragma unroll
+  for (int c = 0; c < kCls; ++c) cnt[c] = 0;
   for (int p = p0; p < p1; ++p) ++cnt[cls(logical(p))];
   // exclusive scan of the per-thread counts of every class over the block, in thread order
   int pre[kCls];
@@ -2585,7 +2596,8 @@ int run(rm_context* ctx, const Call& c) {
       if (ctx->cost_valid && ctx->cost_key == key) {
         if (!ctx->cost_order) RM_HIP(ctx, hipMalloc(&ctx->cost_order, sizeof(int) * kMaxBlocksPerLaunch));
         hipLaunchKernelGGL(rm_order_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const float*)P, a.rec, Mpad,
-                           (int)nb, (const int*)ctx->block_order, a.order_views, a.order_tiles, ctx->cost_order);
+                           (int)nb, (const int*)ctx->block_order, a.order_views, a.order_tiles, a.steps,
+                           ctx->cost_order);
         RM_HIP(ctx, hipGetLastError());
         a.cost_order = ctx->cost_order;
       }
