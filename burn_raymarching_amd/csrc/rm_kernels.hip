@@ -2180,7 +2180,11 @@ __global__ __launch_bounds__(1024) void rm_order_kernel(const float* __restrict_
   auto cls = [&](int blk) {  // 0: the dearest blocks
     const float cost = P[(long long)blk * rec + (long long)Mpad * 12 + 6];
     const int c = (int)(fminf(fmaxf(cost, 0.0f) * cls_scale, (float)(kCls - 1)));
+#ifdef RM_ORDER_CHEAP_FIRST
+    return c;
+#else
     return kCls - 1 - c;
+#endif
   };
   int cnt[kCls];
 #pragma unroll
