@@ -93,6 +93,7 @@ struct KArgs {
   const int* block_order;     // nullable: heavy-first dispatch order of the tiles of a view (ray_block)
   int order_views, order_tiles;
   const int* cost_order;      // nullable: launch position -> block, by the previous launch's cost (rm_order_kernel)
+  float* cost_out;            // nullable: [block] march-step cost of this launch's blocks (for the next order)
   CamBasis cams[RM_MAX_VIEWS_PER_CALL];
   // activated scene
   const float* centers;
@@ -1481,10 +1482,7 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   int* wflag = reinterpret_cast<int*>(L.misc);  // [kWaves] dead flags, [kWaves] steps saved
   float* wscal = L.misc + 8;                     // [kWaves][8]
   {
-    // scalar 6: the wave's cost in march-step units (steps it ran, + kPostCost if it ran the
-    // post-march forward and the backward), for the next call's cost-ordered dispatch
-    const float cost = lane == 0 ? (float)(a.steps - steps_saved + (dead ? 0 : kPostCost)) : 0.0f;
-    const float vals[8] = {gell[0], gell[1], gell[2], gamb, loss, 0.0f, cost, 0.0f};
+    const float vals[8] = {gell[0], gell[1], gell[2], gamb, loss, 0.0f, 0.0f, 0.0f};
     const float red = wave_reduce8(vals, lane);
     if ((lane & 7) == 7) wscal[wave * 8 + (lane >> 3)] = red;
     if (lane == 0) {
@@ -1493,6 +1491,14 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     }
   }
   __syncthreads();
+  if (a.cost_out != nullptr && tid == 0) {
+    // the block's cost in march-step units: steps its waves ran, + kPostCost per wave that runs
+    // the post-march forward and the backward (the next call's cost-ordered dispatch)
+    int cost = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) cost += a.steps - wflag[kWaves + w] + (wflag[w] ? 0 : kPostCost);
+    a.cost_out[blk] = (float)cost;
+  }
   if (a.stats != nullptr && tid == 0) {
     int ex = 0, sv = 0;
 #pragma unroll
@@ -2159,37 +2165,48 @@ __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restri
 
 // Dispatch order by cost: the previous launch over the same views left each block's cost (march
 // steps its waves ran + kPostCost per wave that ran the post-march forward and the backward) in
-// scalar 6 of its partial record. Blocks of similar cost (RM_ORDER_CLASSES classes) are
+// a compact per-block array (KArgs::cost_out). Blocks of similar cost (RM_ORDER_CLASSES classes) are
 // dispatched together -- dearest first, centre-out within a class -- so co-resident blocks
 // finish together (mixing heavy and light blocks costs 9 %, tools/gpu_ab_rep.sh). One block of
 // 1024 threads: a stable counting sort of the centre-out positions by class. Only the dispatch
 // order changes: results are identical.
-__global__ __launch_bounds__(1024) void rm_order_kernel(const float* __restrict__ P, long long rec, int Mpad, int nb,
+__global__ __launch_bounds__(1024) void rm_order_kernel(const float* __restrict__ costs, int nb,
                                                         const int* __restrict__ block_order, int views, int tiles,
                                                         int steps, int* __restrict__ out) {
   constexpr int kCls = RM_ORDER_CLASSES;
   __shared__ int wsum[kCls][16];
   const float cls_scale = (float)kCls / (float)(kWaves * (steps + kPostCost) + 1);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // every thread takes a run of up to kPer consecutive positions; all loads in flight at once
+  constexpr int kPer = (kMaxBlocksPerLaunch + 1023) / 1024;
   const int chunk = (nb + 1023) / 1024;
   const int p0 = min(tid * chunk, nb), p1 = min(p0 + chunk, nb);
-  auto logical = [&](int p) {
+  int blk[kPer], cl[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int p = min(p0 + u, nb - 1);
     const int r = p / views, v = p - r * views;
-    return v * tiles + block_order[r];
-  };
-  auto cls = [&](int blk) {  // 0: the dearest blocks
-    const float cost = P[(long long)blk * rec + (long long)Mpad * 12 + 6];
-    const int c = (int)(fminf(fmaxf(cost, 0.0f) * cls_scale, (float)(kCls - 1)));
-#ifdef RM_ORDER_CHEAP_FIRST
-    return c;
-#else
-    return kCls - 1 - c;
-#endif
-  };
+    blk[u] = v * tiles + block_order[r];
+  }
+  float cost[kPer];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) cost[u] = costs[blk[u]];
   int cnt[kCls];
 #pragma unroll
   for (int c = 0; c < kCls; ++c) cnt[c] = 0;
-  for (int p = p0; p < p1; ++p) ++cnt[cls(logical(p))];
+#pragma unroll
+  for (int u = 0; u < kPer; ++u) {
+    const int c = (int)(fminf(fmaxf(cost[u], 0.0f) * cls_scale, (float)(kCls - 1)));
+#ifdef RM_ORDER_CHEAP_FIRST
+    cl[u] = c;
+#else
+    cl[u] = kCls - 1 - c;  // class 0: the dearest blocks
+#endif
+    if (p0 + u < p1) {
+#pragma unroll
+      for (int k = 0; k < kCls; ++k) cnt[k] += cl[u] == k ? 1 : 0;
+    }
+  }
   // exclusive scan of the per-thread counts of every class over the block, in thread order
   int pre[kCls];
 #pragma unroll
@@ -2204,26 +2221,29 @@ __global__ __launch_bounds__(1024) void rm_order_kernel(const float* __restrict_
     if (lane == 63) wsum[c][wave] = x;
   }
   __syncthreads();
-  int base[kCls], total = 0;
-#pragma unroll
-  for (int c = 0; c < kCls; ++c) {
-    int before = 0, all = 0;
-    for (int w = 0; w < 16; ++w) {
-      before += w < wave ? wsum[c][w] : 0;
-      all += wsum[c][w];
-    }
-    base[c] = total + before + pre[c];
-    total += all;
+  if (tid == 0) {  // start of every (class, wave) run: classes in order, waves in order within
+    int run = 0;
+    for (int c = 0; c < kCls; ++c)
+      for (int w = 0; w < 16; ++w) {
+        const int n = wsum[c][w];
+        wsum[c][w] = run;
+        run += n;
+      }
   }
-  for (int p = p0; p < p1; ++p) {
-    const int blk = logical(p);
-    const int c = cls(blk);
-    int pos = base[0];
+  __syncthreads();
+  int base[kCls];
 #pragma unroll
-    for (int k = 1; k < kCls; ++k) pos = c == k ? base[k] : pos;
-    out[pos] = blk;
+  for (int c = 0; c < kCls; ++c) base[c] = wsum[c][wave] + pre[c];
 #pragma unroll
-    for (int k = 0; k < kCls; ++k) base[k] += c == k ? 1 : 0;
+  for (int u = 0; u < kPer; ++u) {
+    if (p0 + u < p1) {
+      int pos = base[0];
+#pragma unroll
+      for (int k = 1; k < kCls; ++k) pos = cl[u] == k ? base[k] : pos;
+      out[pos] = blk[u];
+#pragma unroll
+      for (int k = 0; k < kCls; ++k) base[k] += cl[u] == k ? 1 : 0;
+    }
   }
 }
 
@@ -2257,6 +2277,7 @@ struct rm_context {
   int* block_order = nullptr;               // centre-out tile order for order_tx x order_ty tiles
   int order_tx = 0, order_ty = 0;
   int* cost_order = nullptr;                // launch position -> block by the previous launch's cost
+  float* cost_buf = nullptr;                // [kMaxBlocksPerLaunch] per-block cost of the last keyed launch
   unsigned long long cost_key = 0;          // geometry of the launch whose partials the workspace holds
   bool cost_valid = false;
 };
@@ -2582,6 +2603,7 @@ int run(rm_context* ctx, const Call& c) {
     a.esc_flags = nullptr;
     a.block_order = nullptr;
     a.cost_order = nullptr;
+    a.cost_out = nullptr;
     const long long npix = (long long)c.W * c.H;
     if (c.cam && a.tiling == 2 && nb > 1 && done % npix == 0 && nr % npix == 0 && nr == nb * kBlock &&
         (c.march->flags & RM_MARCH_NATURAL_ORDER) == 0) {
@@ -2599,14 +2621,18 @@ int run(rm_context* ctx, const Call& c) {
             ((unsigned long long)Mpad << 1) ^ 1ull;
       if (ctx->cost_valid && ctx->cost_key == key) {
         if (!ctx->cost_order) RM_HIP(ctx, hipMalloc(&ctx->cost_order, sizeof(int) * kMaxBlocksPerLaunch));
-        hipLaunchKernelGGL(rm_order_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const float*)P, a.rec, Mpad,
+        hipLaunchKernelGGL(rm_order_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const float*)ctx->cost_buf,
                            (int)nb, (const int*)ctx->block_order, a.order_views, a.order_tiles, a.steps,
                            ctx->cost_order);
         RM_HIP(ctx, hipGetLastError());
         a.cost_order = ctx->cost_order;
       }
     }
-    if (has_rec) {  // this launch's partials replace the workspace's
+    if (key != 0) {  // this launch records its block costs for the next call over the same views
+      if (!ctx->cost_buf) RM_HIP(ctx, hipMalloc(&ctx->cost_buf, sizeof(float) * kMaxBlocksPerLaunch));
+      a.cost_out = ctx->cost_buf;
+    }
+    if (has_rec) {
       ctx->cost_valid = key != 0;
       ctx->cost_key = key;
     }
@@ -2756,12 +2782,13 @@ int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset) {
 
 void rm_destroy(rm_context* ctx) {
   if (!ctx) return;
-  if (ctx->stats_dev || ctx->esc_flags || ctx->rec || ctx->block_order || ctx->cost_order) {
+  if (ctx->stats_dev || ctx->esc_flags || ctx->rec || ctx->block_order || ctx->cost_order || ctx->cost_buf) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stats_dev) (void)hipFree(ctx->stats_dev);
     if (ctx->esc_flags) (void)hipFree(ctx->esc_flags);
     if (ctx->block_order) (void)hipFree(ctx->block_order);
     if (ctx->cost_order) (void)hipFree(ctx->cost_order);
+    if (ctx->cost_buf) (void)hipFree(ctx->cost_buf);
     if (ctx->rec) (void)hipFree(ctx->rec);
   }
   for (auto& pr : ctx->events) {
