@@ -2221,14 +2221,24 @@ __global__ __launch_bounds__(1024) void rm_order_kernel(const float* __restrict_
     if (lane == 63) wsum[c][wave] = x;
   }
   __syncthreads();
-  if (tid == 0) {  // start of every (class, wave) run: classes in order, waves in order within
-    int run = 0;
-    for (int c = 0; c < kCls; ++c)
-      for (int w = 0; w < 16; ++w) {
-        const int n = wsum[c][w];
-        wsum[c][w] = run;
-        run += n;
-      }
+  // start of every (class, wave) run -- classes in order, waves in order within a class: an
+  // exclusive scan of the kCls x 16 run lengths, class-major, by the first kCls * 16 threads
+  static_assert(kCls * 16 <= 1024, "one scan element per thread");
+  __shared__ int wtot[16];
+  {
+    const int i = tid;
+    int x = i < kCls * 16 ? wsum[i >> 4][i & 15] : 0;
+    const int own = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) wtot[wave] = x;
+    __syncthreads();
+    int before = 0;
+    for (int w = 0; w < wave; ++w) before += wtot[w];
+    if (i < kCls * 16) wsum[i >> 4][i & 15] = before + x - own;
   }
   __syncthreads();
   int base[kCls];
