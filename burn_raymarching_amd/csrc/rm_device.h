@@ -32,7 +32,10 @@ constexpr float kPadCenter = 1e15f;      // padding sphere center x: distance ~1
 constexpr float kTMax = 1e15f;
 // A live wave's post-march forward and backward sweeps in march-step units (the cost-ordered
 // dispatch's estimate; tools/bench_parts.py: ~8-10).
-constexpr int kPostCost = 10;
+#ifndef RM_POST_COST
+#define RM_POST_COST 10
+#endif
+constexpr int kPostCost = RM_POST_COST;
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
