@@ -58,7 +58,7 @@
 #define RM_SCHED_BARRIER() ((void)0)
 #endif
 #ifndef RM_ORDER_CLASSES
-#define RM_ORDER_CLASSES 16  // cost classes of the cost-ordered dispatch (rm_order_kernel)
+#define RM_ORDER_CLASSES 16  // cost classes of the cost-ordered dispatch (order_append)
 #endif
 #ifndef RM_BWD_COMB_BUFS
 #define RM_BWD_COMB_BUFS 1  // transposed backward: combine buffers (1 keeps the block's LDS <= 32 KB)
@@ -92,8 +92,14 @@ struct KArgs {
   const int* esc_flags;       // nullable: per-block escape flags of this launch (rm_escape_kernel)
   const int* block_order;     // nullable: heavy-first dispatch order of the tiles of a view (ray_block)
   int order_views, order_tiles;
-  const int* cost_order;      // nullable: launch position -> block, by the previous launch's cost (rm_order_kernel)
-  float* cost_out;            // nullable: [block] march-step cost of this launch's blocks (for the next order)
+  // cost-ordered dispatch: [class][kMaxBlocksPerLaunch] block lists + [class] counts of the
+  // previous launch (read, nullable), of this launch (appended, nullable) and the counts to clear
+  // for the next launch (nullable)
+  const int* olist_r;
+  const int* ocnt_r;
+  int* olist_w;
+  int* ocnt_w;
+  int* ocnt_z;
   CamBasis cams[RM_MAX_VIEWS_PER_CALL];
   // activated scene
   const float* centers;
@@ -990,9 +996,33 @@ __device__ __forceinline__ long long ray_block(const KArgs& a) {
   const int g = b >> 3;
   if ((g + 1) * 8 <= (int)gridDim.x) b = (g << 3) + (((b & 7) + g) & 7);
 #endif
-  if (a.cost_order != nullptr) return a.cost_order[b];
+  if (a.ocnt_r != nullptr) {
+    // position b of the class-major concatenation of the previous launch's lists; every block
+    // reads the same counts, so a short total (never expected) sends all blocks to the static order
+    int tot = 0, cb = -1, base = 0;
+#pragma unroll
+    for (int c = 0; c < RM_ORDER_CLASSES; ++c) {
+      const int n = a.ocnt_r[c];
+      if (cb < 0 && b < tot + n) {
+        cb = c;
+        base = tot;
+      }
+      tot += n;
+    }
+    if (tot == (int)gridDim.x && cb >= 0) return a.olist_r[cb * kMaxBlocksPerLaunch + (b - base)];
+  }
   const int r = b / a.order_views, v = b - r * a.order_views;
   return (long long)v * a.order_tiles + a.block_order[r];
+}
+
+// Appends the block to its cost class's list for the next launch's dispatch order (class 0: the
+// dearest blocks; cost in march-step units, see the hand-off in rm_ray_kernel).
+__device__ __forceinline__ void order_append(const KArgs& a, long long blk, int cost) {
+  constexpr int kCls = RM_ORDER_CLASSES;
+  const float cls_scale = (float)kCls / (float)(kWaves * (a.steps + kPostCost) + 1);
+  const int c = kCls - 1 - (int)fminf((float)cost * cls_scale, (float)(kCls - 1));
+  const int idx = atomicAdd(a.ocnt_w + c, 1);
+  a.olist_w[c * kMaxBlocksPerLaunch + idx] = (int)blk;
 }
 
 // A block of escaping rays: out = 0 (requested outputs), zero gradient partials, and for the
@@ -1123,8 +1153,10 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   // ---- escape skip (RM_MARCH_SKIP_ESCAPED): a block whose rays all provably leave the scene
   // (rm_escape_kernel) gets out = 0 and zero gradients without marching -- exactly what the full
   // computation yields for them, since their silhouette mask is 0 in f32 (see escapes()).
+  if (a.ocnt_z != nullptr && blockIdx.x == 0 && tid < RM_ORDER_CLASSES) a.ocnt_z[tid] = 0;
   if (a.esc_flags != nullptr && a.esc_flags[blk]) {
     if (a.stats != nullptr && tid == 0) atomicAdd(a.stats, 1ull);
+    if (a.ocnt_w != nullptr && tid == 0) order_append(a, blk, 0);
     escaped_block<MODE>(a, L, blk, ri, valid, tid, lane, wave);
     return;
   }
@@ -1491,13 +1523,13 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     }
   }
   __syncthreads();
-  if (a.cost_out != nullptr && tid == 0) {
+  if (a.ocnt_w != nullptr && tid == 0) {
     // the block's cost in march-step units: steps its waves ran, + kPostCost per wave that runs
     // the post-march forward and the backward (the next call's cost-ordered dispatch)
     int cost = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) cost += a.steps - wflag[kWaves + w] + (wflag[w] ? 0 : kPostCost);
-    a.cost_out[blk] = (float)cost;
+    order_append(a, blk, cost);
   }
   if (a.stats != nullptr && tid == 0) {
     int ex = 0, sv = 0;
@@ -2163,100 +2195,6 @@ __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restri
   }
 }
 
-// Dispatch order by cost: the previous launch over the same views left each block's cost (march
-// steps its waves ran + kPostCost per wave that ran the post-march forward and the backward) in
-// a compact per-block array (KArgs::cost_out). Blocks of similar cost (RM_ORDER_CLASSES classes) are
-// dispatched together -- dearest first, centre-out within a class -- so co-resident blocks
-// finish together (mixing heavy and light blocks costs 9 %, tools/gpu_ab_rep.sh). One block of
-// 1024 threads: a stable counting sort of the centre-out positions by class. Only the dispatch
-// order changes: results are identical.
-__global__ __launch_bounds__(1024) void rm_order_kernel(const float* __restrict__ costs, int nb,
-                                                        const int* __restrict__ block_order, int views, int tiles,
-                                                        int steps, int* __restrict__ out) {
-  constexpr int kCls = RM_ORDER_CLASSES;
-  __shared__ int wsum[kCls][16];
-  const float cls_scale = (float)kCls / (float)(kWaves * (steps + kPostCost) + 1);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // every thread takes a run of up to kPer consecutive positions; all loads in flight at once
-  constexpr int kPer = (kMaxBlocksPerLaunch + 1023) / 1024;
-  const int chunk = (nb + 1023) / 1024;
-  const int p0 = min(tid * chunk, nb), p1 = min(p0 + chunk, nb);
-  int blk[kPer], cl[kPer];
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int p = min(p0 + u, nb - 1);
-    const int r = p / views, v = p - r * views;
-    blk[u] = v * tiles + block_order[r];
-  }
-  float cost[kPer];
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) cost[u] = costs[blk[u]];
-  int cnt[kCls];
-#pragma unroll
-  for (int c = 0; c < kCls; ++c) cnt[c] = 0;
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    const int c = (int)(fminf(fmaxf(cost[u], 0.0f) * cls_scale, (float)(kCls - 1)));
-#ifdef RM_ORDER_CHEAP_FIRST
-    cl[u] = c;
-#else
-    cl[u] = kCls - 1 - c;  // class 0: the dearest blocks
-#endif
-    if (p0 + u < p1) {
-#pragma unroll
-      for (int k = 0; k < kCls; ++k) cnt[k] += cl[u] == k ? 1 : 0;
-    }
-  }
-  // exclusive scan of the per-thread counts of every class over the block, in thread order
-  int pre[kCls];
-#pragma unroll
-  for (int c = 0; c < kCls; ++c) {
-    int x = cnt[c];
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(x, off);
-      if (lane >= off) x += y;
-    }
-    pre[c] = x - cnt[c];
-    if (lane == 63) wsum[c][wave] = x;
-  }
-  __syncthreads();
-  // start of every (class, wave) run -- classes in order, waves in order within a class: an
-  // exclusive scan of the kCls x 16 run lengths, class-major, by the first kCls * 16 threads
-  static_assert(kCls * 16 <= 1024, "one scan element per thread");
-  __shared__ int wtot[16];
-  {
-    const int i = tid;
-    int x = i < kCls * 16 ? wsum[i >> 4][i & 15] : 0;
-    const int own = x;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(x, off);
-      if (lane >= off) x += y;
-    }
-    if (lane == 63) wtot[wave] = x;
-    __syncthreads();
-    int before = 0;
-    for (int w = 0; w < wave; ++w) before += wtot[w];
-    if (i < kCls * 16) wsum[i >> 4][i & 15] = before + x - own;
-  }
-  __syncthreads();
-  int base[kCls];
-#pragma unroll
-  for (int c = 0; c < kCls; ++c) base[c] = wsum[c][wave] + pre[c];
-#pragma unroll
-  for (int u = 0; u < kPer; ++u) {
-    if (p0 + u < p1) {
-      int pos = base[0];
-#pragma unroll
-      for (int k = 1; k < kCls; ++k) pos = cl[u] == k ? base[k] : pos;
-      out[pos] = blk[u];
-#pragma unroll
-      for (int k = 0; k < kCls; ++k) base[k] += cl[u] == k ? 1 : 0;
-    }
-  }
-}
-
 __global__ void rm_sum_small(const float* __restrict__ parts, int n, float* __restrict__ out) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     float acc = 0.0f;
@@ -2286,9 +2224,10 @@ struct rm_context {
   long long stats_blocks = 0;               // ray blocks launched while stats are on
   int* block_order = nullptr;               // centre-out tile order for order_tx x order_ty tiles
   int order_tx = 0, order_ty = 0;
-  int* cost_order = nullptr;                // launch position -> block by the previous launch's cost
-  float* cost_buf = nullptr;                // [kMaxBlocksPerLaunch] per-block cost of the last keyed launch
-  unsigned long long cost_key = 0;          // geometry of the launch whose partials the workspace holds
+  int* olist = nullptr;                     // cost-ordered dispatch: 3 x [class][kMaxBlocksPerLaunch] block lists
+  int* ocnt = nullptr;                      // 3 x [class] list lengths (zeroed one launch ahead)
+  int oturn = 0;                            // the list set the next keyed launch appends to
+  unsigned long long cost_key = 0;          // geometry of the last keyed launch (its lists order the next)
   bool cost_valid = false;
 };
 
@@ -2612,8 +2551,11 @@ int run(rm_context* ctx, const Call& c) {
     if (ctx->stats_dev) ctx->stats_blocks += nb;
     a.esc_flags = nullptr;
     a.block_order = nullptr;
-    a.cost_order = nullptr;
-    a.cost_out = nullptr;
+    a.olist_r = nullptr;
+    a.ocnt_r = nullptr;
+    a.olist_w = nullptr;
+    a.ocnt_w = nullptr;
+    a.ocnt_z = nullptr;
     const long long npix = (long long)c.W * c.H;
     if (c.cam && a.tiling == 2 && nb > 1 && done % npix == 0 && nr % npix == 0 && nr == nb * kBlock &&
         (c.march->flags & RM_MARCH_NATURAL_ORDER) == 0) {
@@ -2629,18 +2571,24 @@ int run(rm_context* ctx, const Call& c) {
         (c.march->flags & RM_MARCH_STATIC_ORDER) == 0) {
       key = ((unsigned long long)c.W << 48) ^ ((unsigned long long)c.H << 32) ^ ((unsigned long long)c.views << 24) ^
             ((unsigned long long)Mpad << 1) ^ 1ull;
-      if (ctx->cost_valid && ctx->cost_key == key) {
-        if (!ctx->cost_order) RM_HIP(ctx, hipMalloc(&ctx->cost_order, sizeof(int) * kMaxBlocksPerLaunch));
-        hipLaunchKernelGGL(rm_order_kernel, dim3(1), dim3(1024), 0, ctx->stream, (const float*)ctx->cost_buf,
-                           (int)nb, (const int*)ctx->block_order, a.order_views, a.order_tiles, a.steps,
-                           ctx->cost_order);
-        RM_HIP(ctx, hipGetLastError());
-        a.cost_order = ctx->cost_order;
+      constexpr int kCls = RM_ORDER_CLASSES;
+      if (!ctx->olist) {
+        RM_HIP(ctx, hipMalloc(&ctx->olist, sizeof(int) * 3 * kCls * kMaxBlocksPerLaunch));
+        RM_HIP(ctx, hipMalloc(&ctx->ocnt, sizeof(int) * 3 * kCls));
+        RM_HIP(ctx, hipMemsetAsync(ctx->ocnt, 0, sizeof(int) * 3 * kCls, ctx->stream));
+        ctx->oturn = 0;
       }
-    }
-    if (key != 0) {  // this launch records its block costs for the next call over the same views
-      if (!ctx->cost_buf) RM_HIP(ctx, hipMalloc(&ctx->cost_buf, sizeof(float) * kMaxBlocksPerLaunch));
-      a.cost_out = ctx->cost_buf;
+      // three list sets in rotation: the previous launch's (read), this launch's (appended;
+      // cleared by the previous launch) and the next launch's (cleared by this one)
+      const int wi = ctx->oturn, ri = (wi + 2) % 3, zi = (wi + 1) % 3;
+      if (ctx->cost_valid && ctx->cost_key == key) {
+        a.olist_r = ctx->olist + (size_t)ri * kCls * kMaxBlocksPerLaunch;
+        a.ocnt_r = ctx->ocnt + ri * kCls;
+      }
+      a.olist_w = ctx->olist + (size_t)wi * kCls * kMaxBlocksPerLaunch;
+      a.ocnt_w = ctx->ocnt + wi * kCls;
+      a.ocnt_z = ctx->ocnt + zi * kCls;
+      ctx->oturn = zi;
     }
     if (has_rec) {
       ctx->cost_valid = key != 0;
@@ -2792,13 +2740,13 @@ int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset) {
 
 void rm_destroy(rm_context* ctx) {
   if (!ctx) return;
-  if (ctx->stats_dev || ctx->esc_flags || ctx->rec || ctx->block_order || ctx->cost_order || ctx->cost_buf) {
+  if (ctx->stats_dev || ctx->esc_flags || ctx->rec || ctx->block_order || ctx->olist) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stats_dev) (void)hipFree(ctx->stats_dev);
     if (ctx->esc_flags) (void)hipFree(ctx->esc_flags);
     if (ctx->block_order) (void)hipFree(ctx->block_order);
-    if (ctx->cost_order) (void)hipFree(ctx->cost_order);
-    if (ctx->cost_buf) (void)hipFree(ctx->cost_buf);
+    if (ctx->olist) (void)hipFree(ctx->olist);
+    if (ctx->ocnt) (void)hipFree(ctx->ocnt);
     if (ctx->rec) (void)hipFree(ctx->rec);
   }
   for (auto& pr : ctx->events) {

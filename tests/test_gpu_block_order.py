@@ -63,7 +63,7 @@ def test_forward_and_backward_identical_in_any_dispatch_order(mods, monkeypatch)
 
 def test_cost_ordered_dispatch_identical(mods, monkeypatch):
     """Cost-ordered dispatch (default for repeated train/backward calls over the same views; the
-    order comes from the previous call's live waves per block, RM_MARCH_STATIC_ORDER / env
+    order comes from the block lists the previous call appended to by cost class, RM_MARCH_STATIC_ORDER / env
     RM_STATIC_ORDER=1 turns it off): the second call of a pair uses it, and its images, loss and
     gradients equal (==) the static centre-out order's."""
     torch, model, render = mods
@@ -81,11 +81,15 @@ def test_cost_ordered_dispatch_identical(mods, monkeypatch):
     l0, g0, o0 = run()
     monkeypatch.setenv("RM_STATIC_ORDER", "0")
     run()                  # establishes the cost history
-    l1, g1, o1 = run()     # dispatched by cost
-    assert torch.equal(o0, o1)
-    assert torch.equal(l0, l1)
-    for key in g0:
-        assert torch.equal(g0[key], g1[key]), key
+    for i in range(4):     # dispatched by cost; the block lists rotate through three sets
+        if i == 2:         # a call over other views in between: its lists must not be used here
+            render.train_step_camera(cams[:2], 128, 128, tgt[:2 * 128 * 128], sc, 32.0, 0.5, 32)
+            run()
+        l1, g1, o1 = run()
+        assert torch.equal(o0, o1)
+        assert torch.equal(l0, l1)
+        for key in g0:
+            assert torch.equal(g0[key], g1[key]), key
     g = torch.randn((4 * 128 * 128, 3), device="cuda", generator=torch.Generator("cuda").manual_seed(3))
     monkeypatch.setenv("RM_STATIC_ORDER", "1")
     b0 = render.render_diff_backward_camera(cams, 128, 128, sc, 32.0, g, 32)
