@@ -60,6 +60,16 @@ def main():
     cams = rmm.ring_cameras(10)
     kl2 = args.k / math.log(2.0)  # base-2 exponent scale
     res = {name: [0, 0] for name in orders}
+    # the conservative test a kernel can run: per row block a bounding sphere (c_b, R_b), per ray
+    # an upper bound D_up = 2 D_prev + ln(M)/k of the hard min (no bound at the first step)
+    bounds = {}
+    for name, o in orders.items():
+        cb = c[o].reshape(-1, 16, 3)
+        ctr = 0.5 * (cb.max(1) + cb.min(1))
+        rb = (np.linalg.norm(cb - ctr[:, None], axis=-1) + r[o].reshape(-1, 16)).max(1)
+        bounds[name] = (ctr, rb)
+    test = {name: [0, 0, 0] for name in orders}  # wave-level, 16-ray-group level, count
+    slack = math.log(args.spheres) / args.k
     alive_steps = 0
     for ti in range(args.tiles):
         eye, tgt, fov = cams[ti % len(cams)]
@@ -67,6 +77,7 @@ def main():
         ty, tx = rng.integers(0, H // 8), rng.integers(0, W // 8)
         dw = d[8 * ty:8 * ty + 8, 8 * tx:8 * tx + 8].reshape(64, 3)
         t = np.zeros(64)
+        Dprev = None
         for st in range(args.steps):
             p = eye + t[:, None] * dw
             dist = np.linalg.norm(p[:, None, :] - c[None], axis=-1) - r[None]  # [64, M]
@@ -82,10 +93,20 @@ def main():
                 skip = np.all(blk < -args.thr, axis=0)
                 res[name][0] += int(skip.sum())
                 res[name][1] += skip.size
+            if Dprev is not None:
+                dup = 2 * np.maximum(Dprev, 0) + slack
+                for name, (ctr, rb) in bounds.items():
+                    dist = np.linalg.norm(p[:, None, :] - ctr[None], axis=-1)  # [64, blocks]
+                    ok = dist - rb[None] - dup[:, None] > args.thr / kl2
+                    test[name][0] += int(np.all(ok, axis=0).sum())
+                    test[name][1] += int(np.all(ok.reshape(4, 16, -1), axis=1).sum()) / 4
+                    test[name][2] += ok.shape[1]
+            Dprev = D
             t = t + D
     print(f"tiles {args.tiles}, wave-steps alive {alive_steps}, threshold 2^-{args.thr:g}")
     for name, (s, n) in res.items():
-        print(f"  {name:7s} row blocks skippable: {s / max(n, 1):.3f}")
+        print(f"  {name:7s} row blocks skippable: {s / max(n, 1):.3f}; by the bound test: per wave "
+              f"{test[name][0] / max(test[name][2], 1):.3f}, per 16-ray group {test[name][1] / max(test[name][2], 1):.3f}")
 
 
 if __name__ == "__main__":
