@@ -21,7 +21,8 @@ Synthetic data (no datasets offline): scene seed 0 (BASELINE.md "Synthetic input
 
 Extra objects on the JSON line:
   roofline      -- the dominant kernel (rm_ray_kernel<train>) timed with hipEvents on its own
-                   stream inside the timed region; algorithmic FLOP = 16*(S+10)*M per ray
+                   stream inside the timed region (on every 5th step, --timing-every: the
+                   events cost ~0.6 % of a timed step); algorithmic FLOP = 16*(S+10)*M per ray
                     counted only for sphere sweeps that actually ran (waves
                    whose rays all escaped stop early, see early_exit, and the normal is one
                    sweep instead of six; achieved_all_rays counts the full 16*(S+10)*M for
@@ -71,6 +72,10 @@ def parse():
                          "0.03-0.12 up to 256 spheres, 0.02-0.06 up to 1024, 0.01-0.04 beyond)")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
+    ap.add_argument("--kernel-timing", choices=["on", "off"], default="on",
+                    help="hipEvents on the train kernel's dispatch packets (off: no roofline; A/B of their cost)")
+    ap.add_argument("--timing-every", type=int, default=5,
+                    help="time the train kernel on every n-th timed step (the events cost ~0.6 %% per timed step)")
     ap.add_argument("--cpu-sample", type=int, default=262144, help="rays of the CPU baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline: repeat the sample this long")
     ap.add_argument("--skip-escaped", choices=["on", "off"], default="off",
@@ -152,14 +157,18 @@ def main():
         step(i)
     torch.cuda.synchronize()
     ctx.collect_timing(reset=True)
-    ctx.timing(True)
     ctx.stats(True)
     ctx.collect_stats(reset=True)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    every = max(args.timing_every, 1)
+    timed_steps = 0
     for i in range(args.warmup, total_steps):
+        timed = args.kernel_timing == "on" and (i - args.warmup) % every == 0
+        ctx.timing(timed)
+        timed_steps += timed
         step(i)
     torch.cuda.synchronize()
     if dist is not None:
@@ -182,7 +191,7 @@ def main():
         dist.all_reduce(kt, op=dist.ReduceOp.MAX)
         kern_ms = float(kt.item())
     kern_avg_ms = kern_ms / max(launches, 1)  # per launch (one per step unless the step splits)
-    kern_step_ms = kern_ms / args.steps       # per step: the roofline's time base
+    kern_step_ms = kern_ms / max(timed_steps, 1)  # per step: the roofline's time base
 
     value = rays_global * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
@@ -200,6 +209,7 @@ def main():
     sweeps_run = (waves_total - blocks_skipped * 4) * S - st["steps_saved"] + waves_post * 5
     executed_frac = max(0.0, sweeps_run / sweeps_total)
     flops_launch = flop_per_ray * rays_per_rank * executed_frac
+    kern_step_ms = kern_step_ms or float("nan")  # no timed launches (--kernel-timing off)
     achieved_tf = flops_launch / (kern_step_ms * 1e-3) / 1e12
     mpad = (M + 31) // 32 * 32
     blocks = (rays_per_rank + 255) // 256
@@ -216,7 +226,7 @@ def main():
                 traffic_src = os.path.relpath(pmc_path, ROOT)
         except Exception:
             traffic = None
-    roofline = {
+    roofline = None if launches == 0 else {
         "bound": "valu",
         "kernel": "rm_ray_kernel<train,camera>",
         "achieved": round(achieved_tf, 3),
