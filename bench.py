@@ -163,7 +163,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    every = max(args.timing_every, 1)
+    # every n-th step when there are enough to sample (short runs: every step)
+    every = max(args.timing_every, 1) if args.steps >= 4 * max(args.timing_every, 1) else 1
     timed_steps = 0
     for i in range(args.warmup, total_steps):
         timed = args.kernel_timing == "on" and (i - args.warmup) % every == 0
