@@ -103,9 +103,9 @@ typedef struct rm_march {
  * march step fewer per ray. This flag makes every ray evaluate it itself. A/B timing. */
 #define RM_MARCH_PER_RAY_ORIGIN 32
 /* Train / backward calls over the same views (one launch): by default the ray blocks are
- * dispatched grouped by the cost they had in the previous such call (its number of live
- * waves), heaviest first; this flag keeps the static centre-out order. Results are identical
- * either way. A/B timing. */
+ * dispatched grouped by the cost they had in the previous such call (march steps their waves
+ * ran, plus the post-march work of live waves), dearest first; this flag keeps the static
+ * centre-out order. Results are identical either way. A/B timing. */
 #define RM_MARCH_STATIC_ORDER 64
 
 /* Pinhole LookAt camera, camera.rs:30-37. Rays are generated in-kernel exactly as
