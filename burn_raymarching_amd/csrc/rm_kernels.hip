@@ -1022,7 +1022,9 @@ __device__ __forceinline__ void order_append(const KArgs& a, long long blk, int 
   const float cls_scale = (float)kCls / (float)(kWaves * (a.steps + kPostCost) + 1);
   const int c = kCls - 1 - (int)fminf((float)cost * cls_scale, (float)(kCls - 1));
   const int idx = atomicAdd(a.ocnt_w + c, 1);
-  a.olist_w[c * kMaxBlocksPerLaunch + idx] = (int)blk;
+  // counts left uncleared (a failed launch in the rotation) overrun the total, and ray_block
+  // then falls back to the static order: never write past the list
+  if (idx < kMaxBlocksPerLaunch) a.olist_w[c * kMaxBlocksPerLaunch + idx] = (int)blk;
 }
 
 // A block of escaping rays: out = 0 (requested outputs), zero gradient partials, and for the
