@@ -89,6 +89,7 @@ struct KArgs {
   unsigned long long* stats;  // nullable: [0] += 1 per escaped (skipped) block
   float gone_d;               // > 0: waves whose rays all escaped past this distance stop marching
   int mfma;                   // march sums on the matrix cores (lse_mfma) instead of lse_weighted
+  int shift_max;              // RM_MARCH_FORCE_MAX_SHIFT: every march step takes the running-max shift
   const int* esc_flags;       // nullable: per-block escape flags of this launch (rm_escape_kernel)
   const int* block_order;     // nullable: heavy-first dispatch order of the tiles of a view (ray_block)
   int order_views, order_tiles;
@@ -104,6 +105,7 @@ struct KArgs {
   // activated scene
   const float* centers;
   const float* colors;
+  const _Float16* colors_h;  // RM_MARCH_COLOR_F16: the colours as IEEE half [M,3] (colors is then NULL)
   const float* radius;
   const float* light_dir;
   const float* ambient;
@@ -375,12 +377,13 @@ __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __
     const int M = a0.M;
     for (int e = threadIdx.x; e < 3 * M; e += 256) {
       stage[e] = a0.centers[e];
-      stage[3 * M + e] = a0.colors[e];
+      stage[3 * M + e] = a0.colors_h != nullptr ? (float)a0.colors_h[e] : a0.colors[e];
     }
     for (int e = threadIdx.x; e < M; e += 256) stage[6 * M + e] = a0.radius[e];
     __syncthreads();
     a.centers = stage;
     a.colors = stage + 3 * M;
+    a.colors_h = nullptr;
     a.radius = stage + 6 * M;
   }
   const int np = a.Mpad / 2;
@@ -412,9 +415,15 @@ __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __
         cc[h] = cx * cx + cy * cy + cz * cz;
         kr[h] = kappa * r;
         rr[h] = r;
-        cr[h] = a.colors[3 * j];
-        cg[h] = a.colors[3 * j + 1];
-        cb[h] = a.colors[3 * j + 2];
+        if (a.colors_h != nullptr) {  // fp16 colours: widened exactly, blended in fp32
+          cr[h] = (float)a.colors_h[3 * j];
+          cg[h] = (float)a.colors_h[3 * j + 1];
+          cb[h] = (float)a.colors_h[3 * j + 2];
+        } else {
+          cr[h] = a.colors[3 * j];
+          cg[h] = a.colors[3 * j + 1];
+          cb[h] = a.colors[3 * j + 2];
+        }
         w[h] = fexp2(kr[h]);
         wf[h] = fexp2(kr[h] - kr_first);
         rmin = fminf(rmin, r);
@@ -1172,8 +1181,9 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   // |v_j - v_0| = kappa |r_j - r_0 - (rho_j - rho_0)| <= kappa (r_max + |c_j - c_0|); v <= kappa r_max;
   // the weighted form 2^(k r) 2^(-k rho) also needs 2^(-k rho) of the nearest sphere normal:
   // k rho <= 90 + k r_max <= 120
-  const bool shift_fixed_ok = kappa * (rmax + spread) * 1.001f <= 100.0f;
-  const bool shift_none_ok = kappa * rmax * 1.001f <= 30.0f;
+  // (RM_MARCH_FORCE_MAX_SHIFT: neither, every step takes the running maximum -- tests)
+  const bool shift_fixed_ok = !a.shift_max && kappa * (rmax + spread) * 1.001f <= 100.0f;
+  const bool shift_none_ok = !a.shift_max && kappa * rmax * 1.001f <= 30.0f;
   const float kr_first = kappa * a.radius[0];
   // Wave-uniform choice of the clamp-free path from a per-lane lower bound on the distance.
   auto all_safe = [&](float dist_lb) { return __all(dist_lb + rmin >= kSafeRho) != 0; };
@@ -2127,7 +2137,8 @@ __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restri
                                                            const float* __restrict__ pair, int M, int step,
                                                            float lr, float wd, int with_pen,
                                                            float* __restrict__ pen_parts,
-                                                           float* __restrict__ act_out) {
+                                                           float* __restrict__ act_out,
+                                                           _Float16* __restrict__ col_h_out) {
   __shared__ float red[4 * 256];
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int n = 7 * M + 4;
@@ -2189,6 +2200,8 @@ __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restri
     const float xn = x - lr * (mh / (sqrtf(vh) + eps));
     raw_out[i] = xn;
     if (act_out) act_out[i] = activate_elem(xn, i, M);
+    // fp16 colour models (RM_MARCH_COLOR_F16): the next render's colours, rounded to nearest
+    if (col_h_out != nullptr && i >= 3 * M && i < 6 * M) col_h_out[i - 3 * M] = (_Float16)activate_elem(xn, i, M);
   }
   if (pen_parts != nullptr) {
     float v[4] = {pen, 0.0f, 0.0f, 0.0f};
@@ -2457,7 +2470,12 @@ int run(rm_context* ctx, const Call& c) {
   a.org = c.org;
   a.dir = c.dir;
   a.centers = c.scene->centers;
-  a.colors = c.scene->colors;
+  if ((c.march->flags & RM_MARCH_COLOR_F16) != 0) {
+    a.colors = nullptr;
+    a.colors_h = reinterpret_cast<const _Float16*>(c.scene->colors);
+  } else {
+    a.colors = c.scene->colors;
+  }
   a.radius = c.scene->radius;
   a.light_dir = c.scene->light_dir;
   a.ambient = c.scene->ambient;
@@ -2492,6 +2510,7 @@ int run(rm_context* ctx, const Call& c) {
   }
   if ((c.march->flags & RM_MARCH_ROW_ORDER) != 0) a.tiling = 0;
   a.mfma = (c.march->flags & RM_MARCH_VALU_ONLY) == 0;
+  a.shift_max = (c.march->flags & RM_MARCH_FORCE_MAX_SHIFT) != 0;
   if (c.mode == kRender) {  // renderer.rs:27-32, normalised in f32 on the host like the reference
     const float lv[3] = {-0.5f, 0.5f, -1.0f};
     const float len = std::sqrt(lv[0] * lv[0] + lv[1] * lv[1] + lv[2] * lv[2]);
@@ -2513,7 +2532,7 @@ int run(rm_context* ctx, const Call& c) {
       ctx->rec_bytes = need;
     }
     // camera mode: the per-view first march step at the eye, shared by every ray of the view
-    a.origin = (c.cam && (c.march->flags & RM_MARCH_PER_RAY_ORIGIN) == 0)
+    a.origin = (c.cam && (c.march->flags & (RM_MARCH_PER_RAY_ORIGIN | RM_MARCH_FORCE_MAX_SHIFT)) == 0)
                    ? reinterpret_cast<float*>((char*)ctx->rec + origin_offset(np, nprep))
                    : nullptr;
     hipLaunchKernelGGL(rm_prep_kernel, dim3(nprep), dim3(256), 0, ctx->stream, a, (float4*)ctx->rec);
@@ -2590,6 +2609,8 @@ int run(rm_context* ctx, const Call& c) {
       a.olist_w = ctx->olist + (size_t)wi * kCls * kMaxBlocksPerLaunch;
       a.ocnt_w = ctx->ocnt + wi * kCls;
       a.ocnt_z = ctx->ocnt + zi * kCls;
+      if (const char* e = std::getenv("RM_DEBUG_SKIP_ORDER_CLEAR"))  // recovery test (rm_debug_order_counts)
+        if (e[0] == '1') a.ocnt_z = nullptr;
       ctx->oturn = zi;
     }
     if (has_rec) {
@@ -2705,6 +2726,22 @@ int rm_timing_collect(rm_context* ctx, double* total_ms, int64_t* launches, int3
   *total_ms = acc;
   *launches = (int64_t)ctx->events_used;
   if (reset) ctx->events_used = 0;
+  return RM_OK;
+}
+
+int rm_debug_order_counts(rm_context* ctx, int32_t* counts, int32_t capacity, int32_t* classes, int32_t* next_set) {
+  if (!ctx) return RM_ERR_INVALID_ARG;
+  constexpr int kCls = RM_ORDER_CLASSES;
+  if (classes) *classes = kCls;
+  if (next_set) *next_set = ctx->oturn;
+  if (!counts) return RM_OK;
+  if (capacity < 3 * kCls) return fail(ctx, RM_ERR_INVALID_ARG, "counts needs %d entries", 3 * kCls);
+  RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (!ctx->ocnt) {
+    for (int i = 0; i < 3 * kCls; ++i) counts[i] = 0;
+    return RM_OK;
+  }
+  RM_HIP(ctx, hipMemcpy(counts, ctx->ocnt, sizeof(int) * 3 * kCls, hipMemcpyDeviceToHost));
   return RM_OK;
 }
 
@@ -2993,9 +3030,9 @@ void rm_grads_from_packed(float* g, int32_t M, rm_grads* o) {
   o->ambient = g + 7 * M + 3;
 }
 
-int rm_optimizer_step(rm_context* ctx, float* raw_packed, const float* grad_act_packed, float* adam_m,
-                      float* adam_v, int32_t num_spheres, int32_t step, float lr, float weight_decay,
-                      int32_t with_penalties, float* loss_penalty, float* act_out) {
+int rm_optimizer_step_f16(rm_context* ctx, float* raw_packed, const float* grad_act_packed, float* adam_m,
+                          float* adam_v, int32_t num_spheres, int32_t step, float lr, float weight_decay,
+                          int32_t with_penalties, float* loss_penalty, float* act_out, uint16_t* colors_f16_out) {
   if (!ctx) return RM_ERR_INVALID_ARG;
   if (!raw_packed || !grad_act_packed || !adam_m || !adam_v)
     return fail(ctx, RM_ERR_INVALID_ARG, "NULL optimizer buffer");
@@ -3016,13 +3053,20 @@ int rm_optimizer_step(rm_context* ctx, float* raw_packed, const float* grad_act_
   RM_HIP(ctx, hipGetLastError());
   hipLaunchKernelGGL(rm::rm_optimizer_kernel, dim3(nb), dim3(256), 0, ctx->stream, snap, raw_packed,
                      grad_act_packed, adam_m, adam_v, pair, M, step, lr, weight_decay, with_penalties ? 1 : 0, parts,
-                     act_out);
+                     act_out, reinterpret_cast<_Float16*>(colors_f16_out));
   RM_HIP(ctx, hipGetLastError());
   if (loss_penalty) {
     hipLaunchKernelGGL(rm::rm_sum_small, dim3(1), dim3(64), 0, ctx->stream, parts, nb, loss_penalty);
     RM_HIP(ctx, hipGetLastError());
   }
   return RM_OK;
+}
+
+int rm_optimizer_step(rm_context* ctx, float* raw_packed, const float* grad_act_packed, float* adam_m,
+                      float* adam_v, int32_t num_spheres, int32_t step, float lr, float weight_decay,
+                      int32_t with_penalties, float* loss_penalty, float* act_out) {
+  return rm_optimizer_step_f16(ctx, raw_packed, grad_act_packed, adam_m, adam_v, num_spheres, step, lr, weight_decay,
+                               with_penalties, loss_penalty, act_out, nullptr);
 }
 
 }  // extern "C"

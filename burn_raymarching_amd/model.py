@@ -52,24 +52,31 @@ def softplus_inv(y):
 class SceneModel:
     """model/scene.rs:9-57 -- raw parameters on the device; forward renders via HIP."""
 
-    def __init__(self, raw_packed: torch.Tensor, num_spheres: int):
+    def __init__(self, raw_packed: torch.Tensor, num_spheres: int, color_dtype: str = "f32"):
         if raw_packed.numel() != packed_size(num_spheres):
             raise ValueError("packed buffer size does not match num_spheres")
+        if color_dtype not in ("f32", "f16"):
+            raise ValueError("color_dtype must be 'f32' or 'f16'")
         self.raw = raw_packed.contiguous().float()
         self.num_spheres = num_spheres
         self._act = torch.empty_like(self.raw)
         self._act_valid = False  # _act == activate(raw); Adam.step keeps it valid
+        # fp16 colour / fp32 SDF (BASELINE configs[4]): the render reads half colours
+        # (RM_MARCH_COLOR_F16); parameters, moments and gradients stay fp32
+        self.color_f16 = color_dtype == "f16"
+        self._col_h = torch.empty((num_spheres, 3), dtype=torch.float16, device=self.raw.device) \
+            if self.color_f16 else None
 
     @classmethod
-    def from_raw(cls, centers, colors, radius, light_dir, ambient, device="cuda"):
+    def from_raw(cls, centers, colors, radius, light_dir, ambient, device="cuda", color_dtype="f32"):
         buf = pack(centers, colors, radius, light_dir, ambient)
-        return cls(torch.from_numpy(buf).to(device), np.asarray(centers).reshape(-1, 3).shape[0])
+        return cls(torch.from_numpy(buf).to(device), np.asarray(centers).reshape(-1, 3).shape[0], color_dtype)
 
     @classmethod
-    def from_activated(cls, centers, colors, radius, light_dir, ambient, device="cuda"):
+    def from_activated(cls, centers, colors, radius, light_dir, ambient, device="cuda", color_dtype="f32"):
         """Build raw params whose activations equal the given values (radius includes +0.01)."""
         return cls.from_raw(centers, logit(colors), softplus_inv(np.asarray(radius, np.float64) - 0.01), light_dir,
-                            logit(ambient), device=device)
+                            logit(ambient), device=device, color_dtype=color_dtype)
 
     def invalidate(self):
         """Call after modifying ``raw`` outside the optimizer."""
@@ -81,13 +88,19 @@ class SceneModel:
             ctx.check(ctx._lib.rm_scene_activate(ctx.handle, ctypes.c_void_p(self.raw.data_ptr()),
                                                  self.num_spheres, ctypes.c_void_p(self._act.data_ptr())),
                       "rm_scene_activate")
+            if self.color_f16:  # initial fp16 colours (the optimizer writes them from then on)
+                m = self.num_spheres
+                self._col_h.copy_(self._act[3 * m:6 * m].view(m, 3))
             self._act_valid = True
         return self._act
 
     def scene(self) -> Scene:
-        """scene.rs:41-45 activations as an rm_scene view."""
+        """scene.rs:41-45 activations as an rm_scene view (half colours for color_dtype f16)."""
         a = self.activated_packed()
-        return Scene(*[v for v in unpack(a, self.num_spheres).values()])
+        v = unpack(a, self.num_spheres)
+        if self.color_f16:
+            v["colors"] = self._col_h
+        return Scene(*v.values())
 
     def forward_camera(self, cams, width, height, smooth_k, steps=40):
         return render_diff_camera(cams, width, height, self.scene(), smooth_k, steps)
@@ -110,10 +123,16 @@ class Adam:
         self.t += 1
         ctx = context(self.model.raw.device)
         p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
-        ctx.check(ctx._lib.rm_optimizer_step(ctx.handle, p(self.model.raw), p(grad_act_packed), p(self.m), p(self.v),
-                                             self.model.num_spheres, self.t, float(lr), float(self.weight_decay),
-                                             1 if self.with_penalties else 0, p(penalty_out), p(self.model._act)),
-                  "rm_optimizer_step")
+        if self.model.color_f16:  # fp16-colour model: the updated colours also as half
+            ctx.check(ctx._lib.rm_optimizer_step_f16(
+                ctx.handle, p(self.model.raw), p(grad_act_packed), p(self.m), p(self.v), self.model.num_spheres, self.t,
+                float(lr), float(self.weight_decay), 1 if self.with_penalties else 0, p(penalty_out),
+                p(self.model._act), p(self.model._col_h)), "rm_optimizer_step_f16")
+        else:
+            ctx.check(ctx._lib.rm_optimizer_step(
+                ctx.handle, p(self.model.raw), p(grad_act_packed), p(self.m), p(self.v), self.model.num_spheres, self.t,
+                float(lr), float(self.weight_decay), 1 if self.with_penalties else 0, p(penalty_out),
+                p(self.model._act)), "rm_optimizer_step")
         self.model._act_valid = True
 
 

@@ -40,6 +40,8 @@ RM_MARCH_NATURAL_ORDER = 8
 RM_MARCH_VALU_ONLY = 16
 RM_MARCH_PER_RAY_ORIGIN = 32
 RM_MARCH_STATIC_ORDER = 64
+RM_MARCH_FORCE_MAX_SHIFT = 128
+RM_MARCH_COLOR_F16 = 256
 
 
 class RmStats(ctypes.Structure):
@@ -82,6 +84,8 @@ SIGNATURES = {
     "rm_gather_rays": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _P, _P, _P]),
     "rm_debug_intermediates": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.POINTER(RmScene),
                                               ctypes.POINTER(RmMarch), _P]),
+    "rm_debug_order_counts": (ctypes.c_int, [_P, ctypes.POINTER(_I32), _I32, ctypes.POINTER(_I32),
+                                             ctypes.POINTER(_I32)]),
     "rm_timing_enable": (ctypes.c_int, [_P, _I32]),
     "rm_timing_collect": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64), _I32]),
     "rm_stats_enable": (ctypes.c_int, [_P, _I32]),
@@ -90,6 +94,7 @@ SIGNATURES = {
     "rm_scene_from_packed": (None, [_P, _I32, ctypes.POINTER(RmScene)]),
     "rm_grads_from_packed": (None, [_P, _I32, ctypes.POINTER(RmGrads)]),
     "rm_optimizer_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _F, _F, _I32, _P, _P]),
+    "rm_optimizer_step_f16": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _F, _F, _I32, _P, _P, _P]),
 }
 
 _lib = None
@@ -167,6 +172,17 @@ class Context:
         self.check(self._lib.rm_stats_collect(self.handle, ctypes.byref(st), 1 if reset else 0), "rm_stats_collect")
         return {name: getattr(st, name) for name, _ in RmStats._fields_}
 
+    def order_counts(self):
+        """rm_debug_order_counts: ([3][classes] per-class block counts of the cost-order list sets,
+        next_set)."""
+        buf = (_I32 * 256)()
+        cls = _I32()
+        nxt = _I32()
+        self.check(self._lib.rm_debug_order_counts(self.handle, buf, 256, ctypes.byref(cls), ctypes.byref(nxt)),
+                   "rm_debug_order_counts")
+        c = cls.value
+        return [list(buf[i * c:(i + 1) * c]) for i in range(3)], nxt.value
+
     def close(self):
         if getattr(self, "handle", None) is not None and self.handle.value:
             self._lib.rm_destroy(self.handle)
@@ -180,16 +196,18 @@ class Context:
 
 
 def march_params(steps=40, smooth_k=32.0, normal_eps=1e-4, color_sharpness=10.0, mask_sharpness=15.0,
-                 skip_escaped=None) -> RmMarch:
+                 skip_escaped=None, flags=0) -> RmMarch:
     """rm_march; skip_escaped None = the process default (env RM_SKIP_ESCAPED=1, else off);
     env RM_ROW_ORDER=1 adds RM_MARCH_ROW_ORDER (camera-mode row order instead of 16x16 tiles),
     env RM_NO_EARLY_EXIT=1 adds RM_MARCH_NO_EARLY_EXIT, env RM_NATURAL_ORDER=1 adds
     RM_MARCH_NATURAL_ORDER, env RM_VALU_ONLY=1 adds RM_MARCH_VALU_ONLY, env RM_PER_RAY_ORIGIN=1 adds
-    RM_MARCH_PER_RAY_ORIGIN, env RM_STATIC_ORDER=1 adds RM_MARCH_STATIC_ORDER (A/B tests)."""
+    RM_MARCH_PER_RAY_ORIGIN, env RM_STATIC_ORDER=1 adds RM_MARCH_STATIC_ORDER, env RM_FORCE_MAX_SHIFT=1 adds
+    RM_MARCH_FORCE_MAX_SHIFT (A/B tests); `flags` are ORed in."""
     if skip_escaped is None:
         skip_escaped = os.environ.get("RM_SKIP_ESCAPED", "0") == "1"
-    flags = (RM_MARCH_SKIP_ESCAPED if skip_escaped else 0) | (RM_MARCH_ROW_ORDER if os.environ.get("RM_ROW_ORDER") == "1"
-                                                              else 0)
+    flags = int(flags) | (RM_MARCH_SKIP_ESCAPED if skip_escaped else 0)
+    if os.environ.get("RM_ROW_ORDER") == "1":
+        flags |= RM_MARCH_ROW_ORDER
     if os.environ.get("RM_NO_EARLY_EXIT") == "1":
         flags |= RM_MARCH_NO_EARLY_EXIT
     if os.environ.get("RM_NATURAL_ORDER") == "1":
@@ -200,6 +218,8 @@ def march_params(steps=40, smooth_k=32.0, normal_eps=1e-4, color_sharpness=10.0,
         flags |= RM_MARCH_PER_RAY_ORIGIN
     if os.environ.get("RM_STATIC_ORDER") == "1":
         flags |= RM_MARCH_STATIC_ORDER
+    if os.environ.get("RM_FORCE_MAX_SHIFT") == "1":
+        flags |= RM_MARCH_FORCE_MAX_SHIFT
     return RmMarch(int(steps), float(smooth_k), float(normal_eps), float(color_sharpness), float(mask_sharpness),
                    flags)
 

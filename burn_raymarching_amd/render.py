@@ -63,11 +63,22 @@ class Scene:
     def __init__(self, centers, colors, radius, light_dir, ambient):
         m = centers.shape[0]
         self.centers = _f32(centers, (m, 3), "centers")
-        self.colors = _f32(colors, (m, 3), "colors")
+        # fp16 colour / fp32 SDF (BASELINE configs[4]): half colours select RM_MARCH_COLOR_F16
+        self.color_f16 = isinstance(colors, torch.Tensor) and colors.dtype == torch.float16
+        if self.color_f16:
+            if not colors.is_cuda or tuple(colors.shape) != (m, 3):
+                raise ValueError("fp16 colors must be a [M,3] device tensor")
+            self.colors = colors.contiguous()
+        else:
+            self.colors = _f32(colors, (m, 3), "colors")
         self.radius = _f32(radius.reshape(-1), (m,), "radius")
         self.light_dir = _f32(light_dir.reshape(-1), (3,), "light_dir")
         self.ambient = _f32(ambient.reshape(-1), (1,), "ambient")
         self.num_spheres = m
+
+    @property
+    def march_flags(self) -> int:
+        return native.RM_MARCH_COLOR_F16 if self.color_f16 else 0
 
     def c_struct(self) -> RmScene:
         return RmScene(self.centers.data_ptr(), self.colors.data_ptr(), self.radius.data_ptr(),
@@ -94,6 +105,7 @@ def render_diff_forward(ray_org, ray_dir, scene: Scene, smooth_k, steps=40, *, n
     t = torch.empty((n,), device=ray_org.device) if return_t else None
     ctx = context(ray_org.device)
     march = native.march_params(steps, smooth_k, normal_eps, color_sharpness, mask_sharpness)
+    march.flags |= scene.march_flags
     ctx.check(ctx._lib.rm_render_diff(ctx.handle, _ptr(ray_org), _ptr(ray_dir), n, ctypes.byref(scene.c_struct()),
                                       ctypes.byref(march), _ptr(out), _ptr(t)), "rm_render_diff")
     return (out, t) if return_t else out
@@ -111,6 +123,7 @@ def render_diff_backward(ray_org, ray_dir, scene: Scene, smooth_k, grad_out, ste
     g, cg = _grads_like(scene)
     ctx = context(ray_org.device)
     march = native.march_params(steps, smooth_k, normal_eps, color_sharpness, mask_sharpness)
+    march.flags |= scene.march_flags
     ctx.check(ctx._lib.rm_render_diff_backward(ctx.handle, _ptr(ray_org), _ptr(ray_dir), n,
                                                ctypes.byref(scene.c_struct()), ctypes.byref(march), _ptr(grad_out),
                                                _ptr(t_march), ctypes.byref(cg), 0), "rm_render_diff_backward")
@@ -158,6 +171,7 @@ def render_diff_camera(cams, width, height, scene: Scene, smooth_k, steps=40, *,
     t = torch.empty((v * height * width,), device=dev) if return_t else None
     ctx = context(dev)
     march = native.march_params(steps, smooth_k, normal_eps, color_sharpness, mask_sharpness)
+    march.flags |= scene.march_flags
     for i in range(0, v, native.RM_MAX_VIEWS_PER_CALL):
         chunk = cams[i:i + native.RM_MAX_VIEWS_PER_CALL]
         off = i * height * width
@@ -180,6 +194,7 @@ def render_diff_backward_camera(cams, width, height, scene: Scene, smooth_k, gra
     g, cg = _grads_like(scene)
     ctx = context(scene.centers.device)
     march = native.march_params(steps, smooth_k)
+    march.flags |= scene.march_flags
     ctx.check(ctx._lib.rm_render_diff_backward_camera(ctx.handle, native.cameras(cams), len(cams), width, height,
                                                       ctypes.byref(scene.c_struct()), ctypes.byref(march),
                                                       _ptr(grad_out), _ptr(t_march), ctypes.byref(cg), 0),
@@ -201,6 +216,7 @@ def train_step(ray_org, ray_dir, targets, scene: Scene, smooth_k, progress, step
     out = torch.empty((n, 3), device=ray_org.device) if with_out else None
     ctx = context(ray_org.device)
     march = native.march_params(steps, smooth_k)
+    march.flags |= scene.march_flags
     ctx.check(ctx._lib.rm_train_step(ctx.handle, _ptr(ray_org), _ptr(ray_dir), _ptr(targets), n, float(progress),
                                      float(inv_count), ctypes.byref(scene.c_struct()), ctypes.byref(march),
                                      ctypes.byref(cg), _ptr(loss), _ptr(out), 0), "rm_train_step")
@@ -229,6 +245,7 @@ def train_step_camera(cams, width, height, targets, scene: Scene, smooth_k, prog
         loss = torch.zeros((1,), device=scene.centers.device)
     if march is None:
         march = native.march_params(steps, smooth_k)
+    march.flags |= scene.march_flags
     ctx.check(ctx._lib.rm_train_step_camera(ctx.handle, native.cameras(cams), len(cams), width, height, _ptr(targets),
                                             float(progress), float(inv_count), ctypes.byref(scene.c_struct()),
                                             ctypes.byref(march), ctypes.byref(cg), _ptr(loss), _ptr(out),

@@ -107,6 +107,15 @@ typedef struct rm_march {
  * ran, plus the post-march work of live waves), dearest first; this flag keeps the static
  * centre-out order. Results are identical either way. A/B timing. */
 #define RM_MARCH_STATIC_ORDER 64
+/* Testing: every march step takes the running-maximum log-sum-exp shift (the vector path that
+ * follows the reference's exact max, sdf.rs:36-37) instead of the provably safe unshifted /
+ * fixed-shift forms; implies RM_MARCH_PER_RAY_ORIGIN. Results agree to fp32 rounding. */
+#define RM_MARCH_FORCE_MAX_SHIFT 128
+/* fp16 colour / fp32 SDF (BASELINE configs[4]): rm_scene.colors points to IEEE binary16
+ * [M,3] activated colours instead of fp32. The per-call record kernel widens them exactly;
+ * the colour blend, the SDF, the march and every gradient stay fp32 (grads->colors is fp32,
+ * the master gradient). See rm_optimizer_step_f16 for the optimizer side. */
+#define RM_MARCH_COLOR_F16 256
 
 /* Pinhole LookAt camera, camera.rs:30-37. Rays are generated in-kernel exactly as
  * create_camera_rays (camera.rs:41-87): rows y then x, u = x/W*2-1, v = -(y/H*2-1). */
@@ -204,6 +213,15 @@ int rm_gather_rays(rm_context* ctx, const float* ray_org, const float* ray_dir, 
 int rm_debug_intermediates(rm_context* ctx, const float* ray_org, const float* ray_dir, int64_t num_rays,
                            const rm_scene* scene, const rm_march* march, float* dbg);
 
+/* Cost-ordered dispatch state (tests): copies the 3 x classes per-class block counts of the
+ * three list sets (see RM_MARCH_STATIC_ORDER) into counts[0 .. 3*classes) after synchronising
+ * the stream; *classes = the build's class count, *next_set = the set the next keyed launch
+ * appends to (it reads set (next_set + 2) % 3, whose total equals the launch's block count
+ * when the cost order is used and differs when the launch falls back to the static order).
+ * Environment RM_DEBUG_SKIP_ORDER_CLEAR=1 makes a launch leave the next set's counts
+ * uncleared (the state a failed launch in the rotation leaves), for the recovery test. */
+int rm_debug_order_counts(rm_context* ctx, int32_t* counts, int32_t capacity, int32_t* classes, int32_t* next_set);
+
 /* ---- kernel timing (benchmark instrumentation) ------------------------------ */
 /* rm_timing_enable(ctx, 1): every later render / backward / train call records a
  * hipEvent pair around each launch of its main per-ray kernel on the context's
@@ -249,6 +267,14 @@ void rm_grads_from_packed(float* grad_packed, int32_t num_spheres, rm_grads* out
 int rm_optimizer_step(rm_context* ctx, float* raw_packed, const float* grad_act_packed, float* adam_m,
                       float* adam_v, int32_t num_spheres, int32_t step, float lr, float weight_decay,
                       int32_t with_penalties, float* loss_penalty, float* act_out);
+
+/* rm_optimizer_step for fp16-colour models (RM_MARCH_COLOR_F16, BASELINE configs[4]): the
+ * same update (fp32 master parameters, moments and gradient), and colors_f16_out (nullable,
+ * device, [M,3] IEEE binary16) receives the updated activated colours rounded to nearest --
+ * the colour tensor of the next fp16-colour render. */
+int rm_optimizer_step_f16(rm_context* ctx, float* raw_packed, const float* grad_act_packed, float* adam_m,
+                          float* adam_v, int32_t num_spheres, int32_t step, float lr, float weight_decay,
+                          int32_t with_penalties, float* loss_penalty, float* act_out, uint16_t* colors_f16_out);
 
 #ifdef __cplusplus
 }
