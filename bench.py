@@ -4,39 +4,47 @@ train step at 512x512 / 256 spheres / 32 march steps, on 1..8 MI355X (one proces
 
 One timed step = one full training step of the reference loop (train.rs:169-198) on the
 HIP path, per rank:
-  rm_scene_activate          (scene.rs:41-45)
   rm_train_step_camera       (10 512x512 views: in-kernel rays, fused forward + compute_loss
                               seed + analytic backward, fixed-order gradient reduction)
-  all_reduce(grads) [N > 1]  (RCCL over xGMI; 7M+4 floats)
-  rm_optimizer_step          (activation chain rule + training.rs penalties + Burn Adam)
+  all_reduce(grads) [N > 1]  (RCCL over xGMI; 7M+5 floats: gradient + loss)
+  rm_optimizer_step          (activation chain rule + training.rs penalties + Burn Adam, which
+                              also writes the activated parameters of the next step)
 Views shard across ranks (weak scaling: every rank renders its own 10 views of 512x512 per step).
-value = rays of all ranks / max-over-ranks wall time of the K timed steps.
+value = rays of all ranks * K / max-over-ranks wall time of the K timed steps (barrier +
+synchronize on both sides). `value_median` / `ms_per_step_median` use the median over the K
+steps of the per-step hipEvent time (max over ranks per step).
 
---skip-escaped on (off by default, like the library): ray blocks whose rays provably leave the
-scene with a silhouette mask of exactly 0 get out = 0 and zero gradients without marching --
-bit-identical results (tests/test_gpu_escape.py); `escape_skip` reports the skipped share.
+`--gpus N` without WORLD_SIZE in the environment launches N rank processes itself (one per
+GPU, before anything touches a GPU) and exits with the first failing rank's status; under
+torch.distributed.run the ranks come from the environment, and a WORLD_SIZE that differs from
+--gpus is an error.
 
 Synthetic data (no datasets offline): scene seed 0 (BASELINE.md "Synthetic inputs"), targets
 = the seed-1 scene rendered by the forward kernel from a ring of cameras at radius 2.5, y 0.5.
 
 Extra objects on the JSON line:
-  roofline      -- the dominant kernel (rm_ray_kernel<train>) timed with hipEvents on its own
-                   stream inside the timed region (on every 5th step, --timing-every: the
-                   events cost ~0.6 % of a timed step); algorithmic FLOP = 16*(S+10)*M per ray
-                    counted only for sphere sweeps that actually ran (waves
-                   whose rays all escaped stop early, see early_exit, and the normal is one
-                   sweep instead of six; achieved_all_rays counts the full 16*(S+10)*M for
-                   every ray); bound "valu" (fp32 vector);
-                   traffic = HBM bytes per launch from the committed rocprofv3 PMC summary
-                   (profiles/r01_pmc_traffic.json) when present, else null.
-  cpu_baseline  -- the oracle's fp32 reference-order C restatement (OpenMP) on a bounded
-                   strided sample of the same view, rank 0 at N=1 only.
+  roofline      -- the dominant kernel (rm_ray_kernel<train>) timed with hipEvents from its own
+                   dispatch packet inside the timed region (every 5th step, --timing-every);
+                   algorithmic FLOP = 16*(S+10)*M per ray. `achieved`/`frac`
+                   count the sweeps that ran (executed_frac, from the kernel's work counters in an
+                   untimed replay of the timed steps from a snapshot of the training state:
+                   waves whose rays all escaped stop early, and the normal is one sweep instead of
+                   six); `canonical` is the full 16*(S+10)*M per ray over the kernel time of a
+                   second replay with the early exit off; `pmc` quotes the committed rocprofv3 SQ summary
+                   (profiles/r*_pmc_sq.json) for this workload; traffic = HBM bytes per launch from
+                   the committed FETCH_SIZE / WRITE_SIZE summary (profiles/r*_pmc_traffic.json).
+  cpu_baseline  -- the oracle's fp32 reference-order C restatement (OpenMP) on a bounded strided
+                   sample of the same view, rank 0 at N=1 only: at the box's CPU share (value)
+                   and on one core.
 """
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -50,6 +58,7 @@ METRIC = "Mrays/s fwd+bwd, 512x512 / 256 spheres / 32 steps, at 1/2/4/8 MI355X"
 PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md chip table (vector fp32, spec)
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 FLOP_PER_EVAL = 16         # SURVEY.md §8d canonical count (sqrt and exp counted as 1)
+BYTES_PER_RAY_CAMERA = 24  # SURVEY.md §8d algorithmic HBM bytes per ray, camera mode
 
 
 def parse():
@@ -70,12 +79,17 @@ def parse():
     ap.add_argument("--radius-range", type=float, nargs=2, default=None,
                     help="activated radii U[lo, hi] of the synthetic scenes (default per SURVEY.md 8d: "
                          "0.03-0.12 up to 256 spheres, 0.02-0.06 up to 1024, 0.01-0.04 beyond)")
+    ap.add_argument("--color-dtype", choices=["f32", "f16"], default="f32",
+                    help="f16: fp16 colour / fp32 SDF (BASELINE configs[4], RM_MARCH_COLOR_F16)")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--kernel-timing", choices=["on", "off"], default="on",
                     help="hipEvents on the train kernel's dispatch packets (off: no roofline; A/B of their cost)")
     ap.add_argument("--timing-every", type=int, default=5,
                     help="time the train kernel on every n-th timed step (the events cost ~0.6 %% per timed step)")
+    ap.add_argument("--aux-steps", type=int, default=1,
+                    help="1: replay the timed steps untimed twice after the timed region (work statistics; early "
+                         "exit off for the canonical kernel time); 0: no replays (PMC passes)")
     ap.add_argument("--cpu-sample", type=int, default=262144, help="rays of the CPU baseline sample")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline: repeat the sample this long")
     ap.add_argument("--skip-escaped", choices=["on", "off"], default="off",
@@ -83,14 +97,64 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """One child process per GPU (this process never touches a GPU). Returns the first nonzero
+    exit status, terminating the other ranks when one fails."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def _latest_profile(pattern: str, key: str, field: str):
+    """(value, relative path) of `field`[key] in the newest committed profile matching pattern."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", pattern)), reverse=True):
+        try:
+            data = json.load(open(path))
+        except (OSError, ValueError):
+            continue
+        if key in data.get(field, {}):
+            return data[field][key], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and not (world == 1 and args.gpus == 1):
-        if rank == 0:
-            print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+    if world != args.gpus:
+        print(f"error: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+        sys.exit(2)
+    if os.environ.get("RM_BENCH_RANK_PROBE") == "1":  # launcher test (CPU): report the rank layout, no GPU
+        print(json.dumps({"rank": rank, "local_rank": local, "world": world,
+                          "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
+        return
 
     import torch
     torch.cuda.set_device(local)
@@ -100,8 +164,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from burn_raymarching_amd import model as rmm
-    from burn_raymarching_amd import render as rmr
     from burn_raymarching_amd import native
+    from burn_raymarching_amd import render as rmr
     from burn_raymarching_amd.parallel import Shard, ViewShardedStep
 
     W, H, M, S, K = args.width, args.height, args.spheres, args.march_steps, args.smooth_k
@@ -125,7 +189,7 @@ def main():
         chunk = cams[v0:v0 + native.RM_MAX_VIEWS_PER_CALL]
         targets[v0:v0 + len(chunk)] = rmr.render_diff_camera(chunk, W, H, tgt_scene, K, S).view(len(chunk), npix, 3)
     model = rmm.SceneModel.from_activated(sc0["centers"], sc0["colors"], sc0["radius"], sc0["light_dir"],
-                                          sc0["ambient"])
+                                          sc0["ambient"], color_dtype=args.color_dtype)
     opt = rmm.Adam(model, weight_decay=1e-5, with_penalties=True)
     march = native.march_params(S, K, skip_escaped=args.skip_escaped == "on")
     ctx = rmr.context()
@@ -142,7 +206,7 @@ def main():
         assert views == [(first + j) % ring for j in range(len(views))]
         tg = targets2[first:first + len(views)]
         rmr.train_step_camera([cams[j] for j in views], W, H, tg.view(-1, 3), model.scene(), K,
-                              progress=progress["i"] / total_steps, steps=S, inv_count=inv_count,
+                              progress=min(progress["i"] / total_steps, 1.0), steps=S, inv_count=inv_count,
                               grads_packed=grads_out, loss=loss_out, march=march)
 
     dp = ViewShardedStep(Shard(rank, world, vpg, ring), npix, rmm.packed_size(M), "cuda", step_fn,
@@ -155,42 +219,85 @@ def main():
 
     for i in range(args.warmup):
         step(i)
+    # snapshot of the training state at the start of the timed region (for the untimed replays)
+    snap = (model.raw.clone(), model._act.clone(), opt.m.clone(), opt.v.clone(), opt.t,
+            None if model._col_h is None else model._col_h.clone())
+
+    def restore():
+        model.raw.copy_(snap[0])
+        model._act.copy_(snap[1])
+        opt.m.copy_(snap[2])
+        opt.v.copy_(snap[3])
+        opt.t = snap[4]
+        if snap[5] is not None:
+            model._col_h.copy_(snap[5])
+        model._act_valid = True
+
     torch.cuda.synchronize()
     ctx.collect_timing(reset=True)
-    ctx.stats(True)
-    ctx.collect_stats(reset=True)
+    # every n-th step when there are enough to sample (short runs: every step)
+    every = max(args.timing_every, 1) if args.steps >= 4 * max(args.timing_every, 1) else 1
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    # every n-th step when there are enough to sample (short runs: every step)
-    every = max(args.timing_every, 1) if args.steps >= 4 * max(args.timing_every, 1) else 1
     timed_steps = 0
-    for i in range(args.warmup, total_steps):
-        timed = args.kernel_timing == "on" and (i - args.warmup) % every == 0
+    for j, i in enumerate(range(args.warmup, total_steps)):
+        timed = args.kernel_timing == "on" and j % every == 0
         ctx.timing(timed)
         timed_steps += timed
+        ev[j][0].record()
         step(i)
+        ev[j][1].record()
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     ctx.timing(False)
     kern_ms, launches = ctx.collect_timing(reset=True)
-    st = ctx.collect_stats(reset=True)
-    ctx.stats(False)
+    step_ms = torch.tensor([a.elapsed_time(b) for a, b in ev], dtype=torch.float64, device="cuda")
+
+    # ---- untimed replays of the timed steps: work statistics, then the canonical kernel time.
+    # The training state was snapshotted before the timed region; every step is deterministic,
+    # so a replay repeats the timed steps' work exactly (same scenes, same rays).
+    def replay(fn_before):
+        restore()
+        for j, i in enumerate(range(args.warmup, total_steps)):
+            fn_before(j)
+            step(i)
+        torch.cuda.synchronize()
+
+    st = {"blocks": 0, "blocks_skipped": 0, "waves": 0, "waves_exited": 0, "steps_saved": 0}
+    canon_ms = None
+    if args.aux_steps > 0:
+        ctx.stats(True)
+        ctx.collect_stats(reset=True)
+        replay(lambda j: None)
+        st = ctx.collect_stats(reset=True)
+        ctx.stats(False)
+        if args.kernel_timing == "on":  # the same steps with the early exit off (full work per ray)
+            march.flags |= native.RM_MARCH_NO_EARLY_EXIT
+            ctx.collect_timing(reset=True)
+            replay(lambda j: ctx.timing(j % every == 0 and j > 0))
+            ctx.timing(False)
+            cms, cl = ctx.collect_timing(reset=True)
+            canon_ms = cms / cl if cl else None
+            march.flags &= ~native.RM_MARCH_NO_EARLY_EXIT
+
+    if dist is not None:
+        t = torch.tensor([elapsed, kern_ms, canon_ms or 0.0], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms, canon_ms = float(t[0]), float(t[1]), (float(t[2]) or None)
+        dist.all_reduce(step_ms, op=dist.ReduceOp.MAX)
+    step_ms = step_ms.cpu().numpy()
+    med_ms = float(np.median(step_ms))
+
     blocks_run, blocks_skipped = st["blocks"], st["blocks_skipped"]
     skipped_frac = blocks_skipped / max(blocks_run, 1)
     # march steps not run: whole skipped blocks plus waves that left the march early
     waves_total = max(st["waves"], 1)
     march_saved_frac = (blocks_skipped * 4 * S + st["steps_saved"]) / (waves_total * S)
-    if dist is not None:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        kt = torch.tensor([kern_ms], device="cuda", dtype=torch.float64)
-        dist.all_reduce(kt, op=dist.ReduceOp.MAX)
-        kern_ms = float(kt.item())
     kern_avg_ms = kern_ms / max(launches, 1)  # per launch (one per step unless the step splits)
     kern_step_ms = kern_ms / max(timed_steps, 1)  # per step: the roofline's time base
 
@@ -208,32 +315,31 @@ def main():
     sweeps_total = waves_total * (S + 10)
     waves_post = max(waves_total - blocks_skipped * 4 - st["waves_exited"], 0)
     sweeps_run = (waves_total - blocks_skipped * 4) * S - st["steps_saved"] + waves_post * 5
-    executed_frac = max(0.0, sweeps_run / sweeps_total)
-    flops_launch = flop_per_ray * rays_per_rank * executed_frac
+    have_stats = st["waves"] > 0  # --aux-steps 0 (PMC passes): no statistics, no executed-work figure
+    executed_frac = max(0.0, sweeps_run / sweeps_total) if have_stats else None
     kern_step_ms = kern_step_ms or float("nan")  # no timed launches (--kernel-timing off)
-    achieved_tf = flops_launch / (kern_step_ms * 1e-3) / 1e12
+    achieved_tf = (flop_per_ray * rays_per_rank * executed_frac / (kern_step_ms * 1e-3) / 1e12
+                   if have_stats else None)
+    key = f"{W}x{H}_M{M}_S{S}_V{vpg}" + ("_c16" if args.color_dtype == "f16" else "")
+    traffic, traffic_src = _latest_profile("r*_pmc_traffic.json", key, "train_kernel_bytes_per_launch")
+    pmc, pmc_src = _latest_profile("r*_pmc_sq.json", key, "train_kernel")
+    alg_bytes = rays_per_rank * BYTES_PER_RAY_CAMERA
     mpad = (M + 31) // 32 * 32
-    blocks = (rays_per_rank + 255) // 256
-    alg_bytes = rays_per_rank * 12 + blocks * (mpad * 12 + 8) * 4  # target read + partial-gradient slabs
-    traffic = None
-    traffic_src = None
-    pmc_path = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")  # committed rocprofv3 PMC summary
-    if os.path.exists(pmc_path):
-        try:
-            pmc = json.load(open(pmc_path))
-            key = f"{W}x{H}_M{M}_S{S}_V{vpg}"
-            if key in pmc.get("train_kernel_bytes_per_launch", {}):
-                traffic = float(pmc["train_kernel_bytes_per_launch"][key])
-                traffic_src = os.path.relpath(pmc_path, ROOT)
-        except Exception:
-            traffic = None
+    slab_bytes = (rays_per_rank + 255) // 256 * (mpad * 12 + 8) * 4  # partial-gradient slabs, if all written
+    canonical = None
+    if canon_ms:
+        ach = flop_per_ray * rays_per_rank / (canon_ms * 1e-3) / 1e12
+        canonical = {"kernel_ms": round(canon_ms, 4), "achieved": round(ach, 3),
+                     "frac": round(ach / PEAK_FP32_TFLOPS, 4),
+                     "note": "full 16*(S+10)*M FLOP per ray over the kernel time of the timed steps replayed "
+                             "untimed with the early exit off"}
     roofline = None if launches == 0 else {
         "bound": "valu",
         "kernel": "rm_ray_kernel<train,camera>",
-        "achieved": round(achieved_tf, 3),
+        "achieved": round(achieved_tf, 3) if have_stats else None,
         "peak": PEAK_FP32_TFLOPS,
         "unit": "TFLOP/s",
-        "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 4),
+        "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 4) if have_stats else None,
         "traffic": traffic,
         "traffic_source": traffic_src,
         "kernel_ms": round(kern_avg_ms, 4),
@@ -241,12 +347,17 @@ def main():
         "launches_timed": launches,
         "flop_per_ray": flop_per_ray,
         "rays_per_launch": rays_per_rank,
-        "executed_frac": round(executed_frac, 4),
+        "executed_frac": round(executed_frac, 4) if have_stats else None,
+        "executed_frac_source": "rm_stats counters, untimed replay of the timed steps",
         "achieved_all_rays": round(flop_per_ray * rays_per_rank / (kern_step_ms * 1e-3) / 1e12, 3),
+        "canonical": canonical,
+        "pmc": None if pmc is None else dict(pmc, source=pmc_src),
         "hbm": {"algorithmic_bytes_per_launch": alg_bytes,
+                "bytes_per_ray": BYTES_PER_RAY_CAMERA,
                 "achieved_GBs": round(alg_bytes / (kern_step_ms * 1e-3) / 1e9, 2),
                 "peak_GBs": PEAK_HBM_GBS,
-                "frac": round(alg_bytes / (kern_step_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 6)},
+                "frac": round(alg_bytes / (kern_step_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, 6),
+                "partial_slab_bytes_max": slab_bytes},
     }
 
     # ---- CPU baseline (rank 0, N = 1 only) -----------------------------------------------
@@ -269,10 +380,15 @@ def main():
             "dtype": "f32",
             "data": "synthetic (seeded scene + targets rendered by the forward kernel)",
             "config": {"workload": f"train step fwd+bwd, {W}x{H} view(s) per GPU, {M} spheres, {S} march steps, "
-                                   f"k={K:g}, camera mode, Adam",
+                                   f"k={K:g}, camera mode, Adam"
+                                   + (", fp16 colour / fp32 SDF" if args.color_dtype == "f16" else ""),
                        "width": W, "height": H, "spheres": M, "march_steps": S, "smooth_k": K,
                        "views_per_gpu": vpg, "rays_per_step": rays_global, "radius_range": list(rr),
+                       "color_storage": args.color_dtype, "sdf_dtype": "f32",
                        "parallelism": f"views-dp{world}"},
+            "value_median": round(rays_global / (med_ms * 1e-3) / 1e6, 3),
+            "ms_per_step_median": round(med_ms, 4),
+            "ms_per_step_min_max": [round(float(step_ms.min()), 4), round(float(step_ms.max()), 4)],
             "roofline": roofline,
             "cpu_baseline": cpu,
             "escape_skip": {"enabled": args.skip_escaped == "on", "blocks": blocks_run,
@@ -283,32 +399,47 @@ def main():
                            "march_steps_saved_frac": round(march_saved_frac, 4)},
             "finite": finite,
         }
-        print(json.dumps(line))
+        print(json.dumps(line), flush=True)
     if dist is not None:
         dist.destroy_process_group()
 
 
 def cpu_baseline(args, sc0, sc1, cam, W, H, M, S, K):
-    """Oracle fp32 reference-order restatement (OpenMP) on a strided sample of the view."""
+    """Oracle fp32 reference-order restatement (OpenMP) on a strided sample of the view: at the
+    CPU share of this box (OMP_NUM_THREADS, else the affinity mask) and on one core."""
     from oracle import oracle as orc
     o, d = orc.camera_rays(W, H, *cam, precision="f32")
-    stride = max(1, (W * H) // max(args.cpu_sample, 1))
-    idx = np.arange(0, W * H, stride)
-    o, d = o[idx], d[idx]
-    tg = orc.render_diff(o, d, sc1, S, K, precision="f32")
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    reps = 0
-    t0 = time.perf_counter()
-    while True:  # repeat the sample until ~10 s of CPU work (bounded: at most 30 repetitions)
-        orc.train_step(o, d, tg, sc0, S, K, 0.5, precision="f32")
-        reps += 1
-        sec = time.perf_counter() - t0
-        if sec >= args.cpu_seconds or reps >= 30:
-            break
-    return {"value": round(reps * len(idx) / sec / 1e6, 6), "unit": "Mrays/s", "cores": threads,
-            "hardware_threads": os.cpu_count(), "kind": "port",
-            "sample": f"{reps} x {len(idx)} rays (every {stride}th pixel of one {W}x{H} view), fwd+bwd train "
-                      f"step, {M} spheres, {S} steps, fp32 reference op order, OpenMP; {sec:.2f} s"}
+    try:
+        share = len(os.sched_getaffinity(0))
+    except AttributeError:
+        share = os.cpu_count() or 1
+    threads = int(os.environ.get("OMP_NUM_THREADS") or share)
+
+    def rate(n_rays, seconds, nthreads):
+        orc.set_threads(nthreads)
+        stride = max(1, (W * H) // max(n_rays, 1))
+        idx = np.arange(0, W * H, stride)
+        oo, dd = o[idx], d[idx]
+        tg = orc.render_diff(oo, dd, sc1, S, K, precision="f32")
+        reps = 0
+        t0 = time.perf_counter()
+        while True:  # repeat the sample for ~`seconds` of CPU work (bounded: at most 30 repetitions)
+            orc.train_step(oo, dd, tg, sc0, S, K, 0.5, precision="f32")
+            reps += 1
+            sec = time.perf_counter() - t0
+            if sec >= seconds or reps >= 30:
+                break
+        return reps * len(idx) / sec / 1e6, reps, len(idx), stride, sec
+
+    v1, r1, n1, s1, t1 = rate(max(args.cpu_sample // 16, 1), max(args.cpu_seconds / 4, 0.05), 1)
+    vn, rn, nn, sn, tn = rate(args.cpu_sample, args.cpu_seconds, threads)
+    return {"value": round(vn, 6), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "single_core_value": round(v1, 6), "hardware_threads": os.cpu_count(), "affinity_cpus": share,
+            "all_hw_threads_linear_estimate": round(v1 * (os.cpu_count() or 1), 4),
+            "sample": f"{rn} x {nn} rays (every {sn}th pixel of one {W}x{H} view) on {threads} threads "
+                      f"({tn:.2f} s) and {r1} x {n1} rays on 1 thread ({t1:.2f} s); fwd+bwd train step, {M} spheres, "
+                      f"{S} steps, fp32 reference op order, OpenMP. The box's CPU share is {threads} threads; "
+                      f"the all-thread figure is a linear estimate, not measured"}
 
 
 if __name__ == "__main__":

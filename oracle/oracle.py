@@ -53,6 +53,16 @@ def lib():
     return _lib
 
 
+def set_threads(n: int) -> int:
+    """OpenMP threads of the oracle's parallel loops; returns the previous setting."""
+    lb = lib()
+    lb.orc_max_threads.restype = ctypes.c_int
+    prev = lb.orc_max_threads()
+    lb.orc_set_threads.argtypes = [ctypes.c_int]
+    lb.orc_set_threads(int(n))
+    return prev
+
+
 def _dt(precision: str):
     if precision == "f32":
         return np.float32

@@ -50,3 +50,8 @@
 #include "rm_oracle_impl.h"
 
 int orc_version(void) { return 1; }
+
+/* OpenMP threads of the parallel loops (bench.py's cpu_baseline times 1 and n threads). */
+#include <omp.h>
+void orc_set_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
+int orc_max_threads(void) { return omp_get_max_threads(); }

@@ -1,0 +1,44 @@
+"""bench.py's rank launcher on CPU (no GPU is touched): `--gpus N` without WORLD_SIZE starts N
+rank processes with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set (one per GPU), and a
+WORLD_SIZE that disagrees with --gpus is an error rather than a silent single-GPU run."""
+import json
+import os
+import subprocess
+import sys
+
+from conftest import ROOT
+
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(kw)
+    return env
+
+
+def test_launcher_starts_one_rank_per_gpu():
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "4"], env=_env(RM_BENCH_RANK_PROBE="1"),
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr
+    ranks = [json.loads(ln) for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert sorted(r["rank"] for r in ranks) == [0, 1, 2, 3]
+    assert all(r["world"] == 4 and r["local_rank"] == r["rank"] for r in ranks)
+    masters = {r["master"] for r in ranks}
+    assert len(masters) == 1 and next(iter(masters)).startswith("127.0.0.1:")
+
+
+def test_world_size_mismatch_is_an_error():
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "8"],
+                         env=_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", RM_BENCH_RANK_PROBE="1"),
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 2 and "WORLD_SIZE=2" in out.stderr
+
+
+def test_failing_rank_fails_the_launch():
+    # an unknown rank layout: RM_BENCH_RANK_PROBE off and no GPU here -> the ranks fail; the
+    # launcher must return nonzero instead of hanging or reporting success
+    env = _env(CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    out = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "1", "--warmup", "0"], env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode != 0
