@@ -1,7 +1,7 @@
 """Build recipe for the in-tree native libraries (hipcc for gfx950; no JIT cache).
 
   burn_raymarching_amd/lib/libraymarch_hip.so  <- csrc/rm_kernels.hip   (the product: C ABI of include/raymarch.h)
-  burn_raymarching_amd/lib/librm_host.so        <- csrc/host/{io,data,driver}.cpp (C ABI of include/rm_host.h)
+  burn_raymarching_amd/lib/librm_host.so        <- csrc/host/{io,data,driver,comm}.cpp (C ABI of include/rm_host.h; RCCL)
   burn_raymarching_amd/lib/rm_train             <- csrc/host/main.cpp    (CLI: train / generate / preview)
 
 Run ``python -m burn_raymarching_amd._build`` or ``__graft_entry__.build()``.
@@ -59,13 +59,13 @@ def build_host(force: bool = False, verbose: bool = False) -> str:
     inc = os.path.join(ROOT, "include")
     headers = [os.path.join(inc, "raymarch.h"), os.path.join(inc, "rm_host.h"),
                os.path.join(host_dir, "rmh_common.hpp")]
-    lib_srcs = [os.path.join(host_dir, f) for f in ("io.cpp", "data.cpp", "driver.cpp")]
+    lib_srcs = [os.path.join(host_dir, f) for f in ("io.cpp", "data.cpp", "driver.cpp", "comm.cpp")]
     # -ffp-contract=off: the host f32 arithmetic (camera rays, prune_and_split) keeps the
     # reference's rounding, no fused multiply-adds
     common = [_hipcc(), "-O2", "-std=c++17", "-Wall", "-fPIC", "-ffp-contract=off", "-I", inc]
     rpath = ["-Wl,-rpath,$ORIGIN"]
     if force or _stale(HOST_LIB, lib_srcs + headers + [lib]):
-        cmd = common + ["-shared", "-o", HOST_LIB] + lib_srcs + ["-L", LIBDIR, "-lraymarch_hip", "-lz"] + rpath
+        cmd = common + ["-shared", "-o", HOST_LIB] + lib_srcs + ["-L", LIBDIR, "-lraymarch_hip", "-lz", "-lrccl"] + rpath
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)

@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 
 #include "raymarch.h"
@@ -156,7 +157,13 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
       cfg->march_steps < 1)
     return fail(RMH_ERR_INVALID_ARG, "bad training configuration");
   const int32_t W = cfg->width, H = cfg->height;
-  const bool verbose = cfg->log_every > 0;
+  const rmh_collective* comm = cfg->comm;
+  const int32_t world = comm ? comm->world : 1, rank = comm ? comm->rank : 0;
+  if (world < 1 || rank < 0 || rank >= world || (world > 1 && (!comm->all_reduce_sum || !comm->broadcast)))
+    return fail(RMH_ERR_INVALID_ARG, "bad collective (rank %d of %d)", rank, world);
+  if (cfg->batch < world) return fail(RMH_ERR_INVALID_ARG, "batch %d < %d ranks", cfg->batch, world);
+  const bool lead = rank == 0;  // logs, previews and scene.json
+  const bool verbose = cfg->log_every > 0 && lead;
 
   // ---- 1. cameras and targets (train.rs:62-96) ----
   rmh_camera_entry* cams = nullptr;
@@ -191,19 +198,20 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
 
   Gpu g;
   if ((rc = g.open(cfg->device)) != RMH_OK) return rc;
-  DevBuf d_org, d_dir, d_tgt, d_idx, b_org, b_dir, b_tgt, d_scalars;
+  DevBuf d_org, d_dir, d_tgt, d_idx, b_org, b_dir, b_tgt;
   HIPCHK(d_org.alloc(sizeof(float) * 3 * P));
   HIPCHK(d_dir.alloc(sizeof(float) * 3 * P));
   HIPCHK(d_tgt.alloc(sizeof(float) * 3 * P));
   HIPCHK(hipMemcpyAsync(d_org.p, h_org.data(), d_org.bytes, hipMemcpyHostToDevice, g.stream));
   HIPCHK(hipMemcpyAsync(d_dir.p, h_dir.data(), d_dir.bytes, hipMemcpyHostToDevice, g.stream));
   HIPCHK(hipMemcpyAsync(d_tgt.p, h_tgt.data(), d_tgt.bytes, hipMemcpyHostToDevice, g.stream));
-  const int32_t B = cfg->batch;
+  // this rank's share of the batch (B/P rays per rank, the remainder spread)
+  auto share = [&](int32_t q) { return cfg->batch / world + (q < cfg->batch % world ? 1 : 0); };
+  const int32_t B = share(rank);
   HIPCHK(d_idx.alloc(sizeof(int32_t) * 2 * (size_t)B));
   HIPCHK(b_org.alloc(sizeof(float) * 3 * (size_t)B));
   HIPCHK(b_dir.alloc(sizeof(float) * 3 * (size_t)B));
   HIPCHK(b_tgt.alloc(sizeof(float) * 3 * (size_t)B));
-  HIPCHK(d_scalars.alloc(sizeof(float) * 2));  // [loss_sum, loss_penalty]
   // double-buffered pinned index staging: step s writes half s%2 after that half's copy retired
   PinnedBuf pin;
   HIPCHK(hipHostMalloc(&pin.p, sizeof(int32_t) * 2 * (size_t)B, hipHostMallocDefault));
@@ -221,7 +229,7 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
   HIPCHK(hipEventRecord(copied[1], g.stream));
 
   rmh_rng rng_sample, rng_split;
-  rmh_rng_seed(&rng_sample, cfg->seed, 1);
+  rmh_rng_seed(&rng_sample, cfg->seed, 1 + 1000 * (uint64_t)rank);  // rank-distinct batches
   rmh_rng_seed(&rng_split, cfg->seed, 2);
 
   // ---- 2. initial model (train.rs:100-126) ----
@@ -245,7 +253,9 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
     DevBuf d_raw, d_act, d_grad, d_m, d_v;
     HIPCHK(d_raw.alloc(sizeof(float) * np));
     HIPCHK(d_act.alloc(sizeof(float) * np));
-    HIPCHK(d_grad.alloc(sizeof(float) * np));
+    // [packed gradient (np) | loss sum | penalty]: the first np + 1 floats are the one all-reduce
+    HIPCHK(d_grad.alloc(sizeof(float) * (np + 2)));
+    float* d_loss = d_grad.f() + np;
     HIPCHK(d_m.alloc(sizeof(float) * np));
     HIPCHK(d_v.alloc(sizeof(float) * np));
     HIPCHK(hipMemcpyAsync(d_raw.p, raw.data(), sizeof(float) * np, hipMemcpyHostToDevice, g.stream));
@@ -272,24 +282,35 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
       HIPCHK(hipEventSynchronize(copied[half]));
       int32_t n = 0;
       if ((rc = rmh_dataset_sample(ds.get(), B, uniform_ratio, &rng_sample, hidx, &n)) != RMH_OK) return rc;
+      // the global ray count of this step (the sampler's count rule per rank: a dataset without
+      // foreground draws only the uniform share, dataset.rs:54-67)
+      int64_t n_global = 0;
+      for (int32_t q = 0; q < world; ++q) {
+        int64_t nq = share(q);
+        if (nfg == 0) nq = std::min<int64_t>(std::max<int64_t>((int64_t)((float)share(q) * uniform_ratio), 0), nq);
+        n_global += nq;
+      }
       int32_t* didx = d_idx.i() + (size_t)half * B;
       HIPCHK(hipMemcpyAsync(didx, hidx, sizeof(int32_t) * n, hipMemcpyHostToDevice, g.stream));
       HIPCHK(hipEventRecord(copied[half], g.stream));
       RMCHK(g.ctx, rm_gather_rays(g.ctx, d_org.f(), d_dir.f(), d_tgt.f(), P, didx, n, b_org.f(), b_dir.f(),
                                   b_tgt.f()));
       // model.forward + compute_loss + backward (train.rs:182-190), mean over the n*3 elements
-      RMCHK(g.ctx, rm_train_step(g.ctx, b_org.f(), b_dir.f(), b_tgt.f(), n, progress, 1.0f / (3.0f * (float)n),
-                                 &sc, &march, &gr, d_scalars.f(), nullptr, 0));
+      const float inv_count = 1.0f / (3.0f * (float)n_global);
+      RMCHK(g.ctx, rm_train_step(g.ctx, b_org.f(), b_dir.f(), b_tgt.f(), n, progress, inv_count, &sc, &march, &gr,
+                                 d_loss, nullptr, 0));
+      if (comm && (rc = comm->all_reduce_sum(comm->state, d_grad.f(), (int64_t)np + 1, g.stream)) != RMH_OK)
+        return fail(rc, "all-reduce of the gradient (stage %d, step %d): %s", stage, step, rmh_last_error());
       const double lr = step > cfg->steps_per_stage / 2 ? base_lr * 0.2 : base_lr;  // train.rs:193-197
       RMCHK(g.ctx, rm_optimizer_step(g.ctx, d_raw.f(), d_grad.f(), d_m.f(), d_v.f(), M, step, (float)lr,
-                                     cfg->weight_decay, 1, d_scalars.f() + 1, d_act.f()));
+                                     cfg->weight_decay, 1, d_loss + 1, d_act.f()));
       ++steps_done;
       const bool last = stage == cfg->stages - 1 && step == cfg->steps_per_stage;
       if ((verbose && step % cfg->log_every == 0) || last) {
         float s[2];
-        HIPCHK(hipMemcpyAsync(s, d_scalars.p, sizeof s, hipMemcpyDeviceToHost, g.stream));
+        HIPCHK(hipMemcpyAsync(s, d_loss, sizeof s, hipMemcpyDeviceToHost, g.stream));
         HIPCHK(hipStreamSynchronize(g.stream));
-        last_loss = s[0] / (3.0f * (float)n) + s[1];  // training.rs:34 + penalties
+        last_loss = s[0] * inv_count + s[1];  // training.rs:34 + penalties
         if (verbose && step % cfg->log_every == 0)
           std::printf("  Step %d | Loss: %.5f | k: %.1f\n", step, last_loss, march.smooth_k);
       }
@@ -299,7 +320,7 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
     HIPCHK(hipMemcpy(raw.data(), d_raw.p, sizeof(float) * np, hipMemcpyDeviceToHost));
 
     if (stage == cfg->stages - 1) {  // train.rs:206-290
-      if (!out_dir.empty()) {
+      if (lead && !out_dir.empty()) {
         if ((rc = export_scene(raw, M, join_path(out_dir, "scene.json"))) != RMH_OK) return rc;
         if (verbose) std::printf("  => Saved to scene.json (N = %d)\n", M);
         if (cfg->previews &&
@@ -308,17 +329,36 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
       }
       break;
     }
-    if (cfg->previews && !out_dir.empty()) {
+    if (lead && cfg->previews && !out_dir.empty()) {
       char name[64];
       std::snprintf(name, sizeof name, "steps/stage_%d.png", stage);
       if ((rc = preview_packed(g, d_act.f(), M, W, H, cfg->march_steps, join_path(out_dir, name)))) return rc;
     }
     // ---- C. prune & split (train.rs:300-328) ----
+    // rank 0 decides the next generation and broadcasts it: its size, then its raw params
     std::vector<float> next(14 * (size_t)M + 4);
     int32_t nextM = 0;
-    if ((rc = rmh_prune_and_split(raw.data(), M, init_centers.data(), stage, cfg->stages, &rng_split, next.data(),
-                                  &nextM)) != RMH_OK)
+    if (lead && (rc = rmh_prune_and_split(raw.data(), M, init_centers.data(), stage, cfg->stages, &rng_split,
+                                          next.data(), &nextM)) != RMH_OK)
       return rc;
+    if (comm) {  // (with one rank too: the RCCL path is the same)
+      DevBuf d_next;
+      HIPCHK(d_next.alloc(sizeof(float) * next.size()));
+      float fm = (float)nextM;  // M' <= 2M <= 2^17: exact in fp32
+      HIPCHK(hipMemcpyAsync(d_next.p, &fm, sizeof fm, hipMemcpyHostToDevice, g.stream));
+      if ((rc = comm->broadcast(comm->state, d_next.f(), 1, 0, g.stream)) != RMH_OK)
+        return fail(rc, "broadcast of the next size: %s", rmh_last_error());
+      HIPCHK(hipMemcpyAsync(&fm, d_next.p, sizeof fm, hipMemcpyDeviceToHost, g.stream));
+      HIPCHK(hipStreamSynchronize(g.stream));
+      nextM = (int32_t)fm;
+      if (nextM < 1 || 7 * (size_t)nextM + 4 > next.size()) return fail(RMH_ERR_GPU, "broadcast size %d", nextM);
+      const size_t nn = 7 * (size_t)nextM + 4;
+      if (lead) HIPCHK(hipMemcpyAsync(d_next.p, next.data(), sizeof(float) * nn, hipMemcpyHostToDevice, g.stream));
+      if ((rc = comm->broadcast(comm->state, d_next.f(), (int64_t)nn, 0, g.stream)) != RMH_OK)
+        return fail(rc, "broadcast of the next generation: %s", rmh_last_error());
+      HIPCHK(hipMemcpyAsync(next.data(), d_next.p, sizeof(float) * nn, hipMemcpyDeviceToHost, g.stream));
+      HIPCHK(hipStreamSynchronize(g.stream));
+    }
     if (nextM > RM_MAX_SPHERES) return fail(RMH_ERR_INVALID_ARG, "model grew past RM_MAX_SPHERES");
     next.resize(7 * (size_t)nextM + 4);
     raw.swap(next);

@@ -3,14 +3,22 @@
 //
 //   rm_train train    [--cameras data/cameras.json] [--out .] [--stages 5] [--steps 700]
 //                     [--batch 16384] [--size 256x256] [--march-steps 40] [--seed 0]
-//                     [--log-every 100] [--no-previews] [--device 0]
+//                     [--log-every 100] [--no-previews] [--device 0] [--ranks N]
+//     --ranks N: data-parallel training on N GPUs (devices 0..N-1), one process per GPU over
+//     RCCL: this process forks the N rank processes before anything touches a GPU and waits
+//     for them. (--rank r --world N --comm-file F run one rank of a run launched elsewhere.)
 //   rm_train generate [--out data] [--prefix data/] [--size 256x256] [--device 0]
 //   rm_train preview  --scene scene.json --png out.png [--size 256x256]
 //                     [--eye 0,0,-2.5] [--target 0,0,0] [--fov 50] [--radius-offset 0.01]
+#include <signal.h>
+#include <sys/wait.h>
+#include <unistd.h>
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <vector>
 
 #include "rm_host.h"
 
@@ -20,7 +28,7 @@ int usage() {
   std::fprintf(stderr,
                "usage: rm_train train|generate|preview [options]\n"
                "  train    --cameras F --out D --stages N --steps N --batch N --size WxH --march-steps N\n"
-               "           --seed N --log-every N --no-previews --device N\n"
+               "           --seed N --log-every N --no-previews --device N --ranks N\n"
                "  generate --out D --prefix P --size WxH --device N\n"
                "  preview  --scene F --png F --size WxH --eye x,y,z --target x,y,z --fov F --radius-offset F\n");
   return 2;
@@ -35,6 +43,70 @@ int report(int rc, const char* what) {
   return rc == RMH_OK ? 0 : 1;
 }
 
+// One rank of a data-parallel run: RCCL communicator, rmh_train, rank 0 prints the result.
+int train_rank(rmh_train_config cfg, int rank, int world, const char* comm_file) {
+  rmh_collective comm;
+  if (world > 1 || rank >= 0) {
+    if (rmh_collective_rccl_create(rank, world, cfg.device, comm_file, 300.0, &comm) != RMH_OK)
+      return report(RMH_ERR_GPU, "train (RCCL)");
+    cfg.comm = &comm;
+  }
+  rmh_train_result res;
+  const int rc = rmh_train(&cfg, &res, nullptr, 0);
+  if (cfg.comm) rmh_collective_rccl_destroy(&comm);
+  if (rc == RMH_OK && rank <= 0)
+    std::printf("{\"num_spheres\": %d, \"steps\": %d, \"final_loss\": %.6g, \"seconds\": %.4f, \"step_ms\": %.4f, "
+                "\"ranks\": %d}\n",
+                res.num_spheres, res.steps, res.final_loss, res.seconds, res.step_ms, world);
+  return report(rc, "train");
+}
+
+// --ranks N: one rank process per GPU (devices 0..N-1), forked before this process touches a
+// GPU (no exec: each child runs its rank directly). Waits for all; when one fails the others
+// are terminated. Returns the first failing exit status (0 if all succeed).
+int launch_ranks(const rmh_train_config& cfg, int n) {
+  char dir[] = "/tmp/rm_train_XXXXXX";
+  if (!mkdtemp(dir)) {
+    std::perror("mkdtemp");
+    return 1;
+  }
+  const std::string id_file = std::string(dir) + "/rccl_id";
+  std::fflush(nullptr);
+  std::vector<pid_t> pids;
+  for (int r = 0; r < n; ++r) {
+    const pid_t pid = fork();
+    if (pid < 0) {
+      std::perror("fork");
+      for (pid_t p : pids) kill(p, SIGTERM);
+      return 1;
+    }
+    if (pid == 0) {
+      rmh_train_config c = cfg;
+      c.device = r;
+      const int code = train_rank(c, r, n, id_file.c_str());
+      std::fflush(nullptr);
+      _exit(code);
+    }
+    pids.push_back(pid);
+  }
+  int rc = 0;
+  for (size_t left = pids.size(); left > 0; --left) {
+    int status = 0;
+    const pid_t p = wait(&status);
+    if (p < 0) break;
+    const int code = WIFEXITED(status) ? WEXITSTATUS(status) : 128 + (WIFSIGNALED(status) ? WTERMSIG(status) : 0);
+    if (code != 0 && rc == 0) {
+      rc = code;
+      for (pid_t q : pids)
+        if (q != p) kill(q, SIGTERM);
+    }
+  }
+  unlink(id_file.c_str());
+  unlink((id_file + ".tmp").c_str());
+  rmdir(dir);
+  return rc;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -44,6 +116,8 @@ int main(int argc, char** argv) {
   if (cmd == "train") {
     rmh_train_config cfg;
     rmh_train_config_default(&cfg);
+    int ranks = 0, rank = -1, world = 1;
+    const char* comm_file = nullptr;
     for (int i = 2; i < argc; ++i) {
       const std::string a = argv[i];
       if (a == "--no-previews") {
@@ -70,16 +144,20 @@ int main(int argc, char** argv) {
         cfg.log_every = std::atoi(argv[++i]);
       } else if (a == "--device") {
         cfg.device = std::atoi(argv[++i]);
+      } else if (a == "--ranks") {
+        ranks = std::atoi(argv[++i]);
+      } else if (a == "--rank") {
+        rank = std::atoi(argv[++i]);
+      } else if (a == "--world") {
+        world = std::atoi(argv[++i]);
+      } else if (a == "--comm-file") {
+        comm_file = argv[++i];
       } else {
         return usage();
       }
     }
-    rmh_train_result res;
-    const int rc = rmh_train(&cfg, &res, nullptr, 0);
-    if (rc == RMH_OK)
-      std::printf("{\"num_spheres\": %d, \"steps\": %d, \"final_loss\": %.6g, \"seconds\": %.4f, \"step_ms\": %.4f}\n",
-                  res.num_spheres, res.steps, res.final_loss, res.seconds, res.step_ms);
-    return report(rc, "train");
+    if (ranks > 0) return launch_ranks(cfg, ranks);
+    return train_rank(cfg, rank, world, comm_file);
   }
   if (cmd == "generate") {
     const char* out = "data";

@@ -32,12 +32,24 @@ class RmhRng(ctypes.Structure):
     _fields_ = [("state", ctypes.c_uint64), ("inc", ctypes.c_uint64)]
 
 
+ALL_REDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p)
+BROADCAST_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                ctypes.c_void_p)
+
+
+class RmhCollective(ctypes.Structure):
+    """rmh_collective: sum all-reduce and broadcast of fp32 device buffers on the driver's stream."""
+    _fields_ = [("state", ctypes.c_void_p), ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
+                ("all_reduce_sum", ALL_REDUCE_FN), ("broadcast", BROADCAST_FN)]
+
+
 class RmhTrainConfig(ctypes.Structure):
     _fields_ = [("cameras_json", ctypes.c_char_p), ("out_dir", ctypes.c_char_p), ("width", ctypes.c_int32),
                 ("height", ctypes.c_int32), ("stages", ctypes.c_int32), ("steps_per_stage", ctypes.c_int32),
                 ("batch", ctypes.c_int32), ("march_steps", ctypes.c_int32), ("max_smooth", ctypes.c_float),
                 ("base_lr", ctypes.c_float), ("weight_decay", ctypes.c_float), ("log_every", ctypes.c_int32),
-                ("previews", ctypes.c_int32), ("seed", ctypes.c_uint64), ("device", ctypes.c_int32)]
+                ("previews", ctypes.c_int32), ("seed", ctypes.c_uint64), ("device", ctypes.c_int32),
+                ("comm", ctypes.POINTER(RmhCollective))]
 
 
 class RmhTrainResult(ctypes.Structure):
@@ -77,6 +89,9 @@ SIGNATURES = {
     "rmh_dataset_sample": (ctypes.c_int, [_P, _I32, _F, ctypes.POINTER(RmhRng), _P, _PI32]),
     "rmh_prune_and_split": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, ctypes.POINTER(RmhRng), _P, _PI32]),
     "rmh_initial_model": (None, [_P]),
+    "rmh_collective_rccl_create": (ctypes.c_int, [_I32, _I32, _I32, _S, ctypes.c_double,
+                                                  ctypes.POINTER(RmhCollective)]),
+    "rmh_collective_rccl_destroy": (None, [ctypes.POINTER(RmhCollective)]),
     "rmh_train_config_default": (None, [ctypes.POINTER(RmhTrainConfig)]),
     "rmh_train": (ctypes.c_int, [ctypes.POINTER(RmhTrainConfig), ctypes.POINTER(RmhTrainResult), _P, _I32]),
     "rmh_preview": (ctypes.c_int, [_S, _S, _I32, _I32, _P, _P, _F, _F, _I32]),
@@ -301,6 +316,37 @@ def train_config(**kw) -> RmhTrainConfig:
             v = None if v is None else _b(v)
         setattr(cfg, k, v)
     return cfg
+
+
+def collective(rank: int, world: int, all_reduce_sum, broadcast) -> RmhCollective:
+    """An rmh_collective over Python callables all_reduce_sum(dev_ptr, count, stream) and
+    broadcast(dev_ptr, count, root, stream) (each returns None or raises). The struct keeps the
+    callbacks alive; keep it alive while rmh_train runs."""
+    def ar(_state, buf, count, stream):
+        try:
+            all_reduce_sum(buf, count, stream)
+            return RMH_OK
+        except Exception as e:  # noqa: BLE001 -- reported through the C status
+            print(f"all_reduce_sum failed: {e!r}")
+            return 4
+    def bc(_state, buf, count, root, stream):
+        try:
+            broadcast(buf, count, root, stream)
+            return RMH_OK
+        except Exception as e:  # noqa: BLE001
+            print(f"broadcast failed: {e!r}")
+            return 4
+    c = RmhCollective(None, rank, world, ALL_REDUCE_FN(ar), BROADCAST_FN(bc))
+    c._keep = (c.all_reduce_sum, c.broadcast)
+    return c
+
+
+def rccl_collective(rank: int, world: int, device: int, id_path: str | None, timeout_s: float = 300.0):
+    """rmh_collective_rccl_create (RCCL over xGMI, one process per GPU)."""
+    c = RmhCollective()
+    _check(lib().rmh_collective_rccl_create(rank, world, device, None if id_path is None else _b(id_path),
+                                            float(timeout_s), ctypes.byref(c)), "rmh_collective_rccl_create")
+    return c
 
 
 def train(cfg: RmhTrainConfig, max_spheres: int = 65536):

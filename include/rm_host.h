@@ -110,6 +110,26 @@ int rmh_prune_and_split(const float* raw_packed, int32_t num_spheres, const floa
 /* The initial 7-sphere raw model of train.rs:100-126 (out: 7*7+4 floats). */
 void rmh_initial_model(float* raw_packed);
 
+/* ---- data-parallel collectives --------------------------------------- */
+/* The two collectives the multi-rank driver issues, on fp32 DEVICE buffers, asynchronously on
+ * the driver's HIP stream (`stream` is a hipStream_t): an in-place sum all-reduce and an
+ * in-place broadcast from `root`. Return RMH_OK or an error code. Any implementation works:
+ * rmh_collective_rccl_create builds the RCCL one (one process per GPU, over xGMI); tests plug
+ * in their own (e.g. gloo over host copies, to run two ranks on one GPU). */
+typedef struct rmh_collective {
+  void* state;
+  int32_t rank;
+  int32_t world;
+  int (*all_reduce_sum)(void* state, float* buf, int64_t count, void* stream);
+  int (*broadcast)(void* state, float* buf, int64_t count, int32_t root, void* stream);
+} rmh_collective;
+/* RCCL communicator of rank `rank` of `world` on HIP device `device`. Rank 0 creates the
+ * ncclUniqueId and publishes it at id_path (write + rename); the other ranks wait for the file
+ * up to timeout_s seconds. id_path may be NULL when world == 1. */
+int rmh_collective_rccl_create(int32_t rank, int32_t world, int32_t device, const char* id_path, double timeout_s,
+                               rmh_collective* out);
+void rmh_collective_rccl_destroy(rmh_collective* c);
+
 /* ---- train.rs: the driver ------------------------------------------------------------- */
 typedef struct rmh_train_config {
   const char* cameras_json; /* data/cameras.json; image paths resolved against its directory */
@@ -126,6 +146,13 @@ typedef struct rmh_train_config {
   int32_t previews;         /* write steps/stage_i.png and steps/final_1.png */
   uint64_t seed;
   int32_t device;
+  /* Data parallelism (NULL: one rank). With comm->world = P ranks each rank samples its share
+   * of the batch (batch / P rays, rank-distinct sampler streams) and runs the fused train step
+   * with the global loss normalisation 1/(3 N_global); one all-reduce(sum) of the packed
+   * [gradient | loss sum] (7M+5 floats) precedes the replicated optimizer step; rank 0 runs
+   * prune_and_split and broadcasts the next generation (its size, then its 7M'+4 raw params);
+   * only rank 0 logs and writes files. Every rank ends with the same parameters. */
+  const rmh_collective* comm;
 } rmh_train_config;
 void rmh_train_config_default(rmh_train_config* cfg);
 

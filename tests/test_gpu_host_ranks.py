@@ -1,0 +1,164 @@
+"""Data-parallel training in the C++ host driver (rmh_train with an rmh_collective, SURVEY.md
+§8(e); the reference's schedule train.rs:138-330 with prune_and_split training.rs:87-238
+between stages).
+
+  * `rm_train train --ranks 1`: the CLI's rank launcher (fork before any GPU use) and the real
+    RCCL communicator (one rank: its all-reduce and broadcasts run on the device);
+  * two rank processes on the test box's one GPU with a gloo collective plugged in through the
+    C ABI (RCCL refuses two ranks on one device; the driver's collective calls are the same):
+    the collective sequence (one all-reduce of 7M+5 floats per step, then per stage transition a
+    broadcast of the size and of the 7M'+4 raw parameters), every reduced buffer = the sum of
+    the ranks' local buffers, broadcasts deliver rank 0's data, and both ranks end with
+    bit-identical parameters;
+  * an identity collective on one rank changes no bit of the single-process run.
+"""
+import ctypes
+import json
+import os
+import socket
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN, ROOT, gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
+
+STAGES, STEPS, BATCH = 2, 40, 4096
+
+
+def _hip():
+    h = ctypes.CDLL("libamdhip64.so")
+    h.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    h.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+    return h
+
+
+def _cfg(H, seed=3):
+    return H.train_config(cameras_json=os.path.join(GOLDEN, "cameras.json"), out_dir=None, log_every=0, previews=0,
+                          stages=STAGES, steps_per_stage=STEPS, batch=BATCH, seed=seed)
+
+
+def _gloo_collective(H, rank, world, log):
+    """rmh_collective over torch.distributed (gloo) on host copies of the device buffers."""
+    import torch
+    import torch.distributed as dist
+    hip = _hip()
+
+    def fetch(buf, count, stream):
+        assert hip.hipStreamSynchronize(stream) == 0
+        a = np.empty(count, np.float32)
+        assert hip.hipMemcpy(a.ctypes.data, buf, 4 * count, 2) == 0  # device -> host
+        return a
+
+    def store(buf, a):
+        assert hip.hipMemcpy(buf, a.ctypes.data, 4 * a.size, 1) == 0  # host -> device
+
+    def all_reduce(buf, count, stream):
+        a = fetch(buf, count, stream)
+        t = torch.from_numpy(a.copy())
+        dist.all_reduce(t)
+        store(buf, t.numpy())
+        log.append(("ar", count, a, t.numpy().copy()))
+
+    def broadcast(buf, count, root, stream):
+        a = fetch(buf, count, stream)
+        t = torch.from_numpy(a.copy())
+        dist.broadcast(t, root)
+        store(buf, t.numpy())
+        log.append(("bc", count, a, t.numpy().copy()))
+
+    return H.collective(rank, world, all_reduce, broadcast)
+
+
+def _worker(rank, world, port, out_dir):
+    import sys
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from burn_raymarching_amd import host as H
+    log = []
+    comm = _gloo_collective(H, rank, world, log)
+    cfg = _cfg(H)
+    cfg.comm = ctypes.pointer(comm)
+    res, raw = H.train(cfg)
+    np.save(os.path.join(out_dir, f"raw{rank}.npy"), raw)
+    seq = [(k, c) for k, c, _, _ in log]
+    json.dump({"seq": seq, "M": res.num_spheres, "steps": res.steps}, open(os.path.join(out_dir, f"r{rank}.json"), "w"))
+    # first and last all-reduce and every broadcast: local (pre) and reduced (post) buffers
+    keep = [i for i, e in enumerate(log) if e[0] == "bc"] + [0, len(log) - 1]
+    np.savez(os.path.join(out_dir, f"bufs{rank}.npz"),
+             **{f"pre{i}": log[i][2] for i in keep}, **{f"post{i}": log[i][3] for i in keep})
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_driver_over_plugged_collective():
+    world = 2
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_worker, args=(world, _free_port(), tmp), nprocs=world, join=True, start_method="spawn")
+        r = [json.load(open(os.path.join(tmp, f"r{q}.json"))) for q in range(world)]
+        raw = [np.load(os.path.join(tmp, f"raw{q}.npy")) for q in range(world)]
+        bufs = [np.load(os.path.join(tmp, f"bufs{q}.npz")) for q in range(world)]
+        assert np.array_equal(raw[0], raw[1])  # replicated parameters stay identical
+        assert r[0]["seq"] == r[1]["seq"] and r[0]["steps"] == STAGES * STEPS
+        seq = r[0]["seq"]
+        # the collective schedule: STEPS all-reduces per stage, a size + params broadcast between
+        kinds = [k for k, _ in seq]
+        assert kinds == (["ar"] * STEPS + ["bc", "bc"]) * (STAGES - 1) + ["ar"] * STEPS
+        assert seq[0][1] == 7 * 7 + 5  # the 7-sphere initial model: gradient + loss sum
+        m_next = None
+        for i, (k, c) in enumerate(seq):
+            if k == "bc" and c == 1:
+                m_next = int(bufs[0][f"post{i}"][0])
+            elif k == "bc":
+                assert c == 7 * m_next + 4
+        assert seq[-1][1] == 7 * r[0]["M"] + 5
+        for key in bufs[0].files:
+            i = int(key[4:]) if key.startswith("post") else None
+            if i is None:
+                continue
+            pre0, pre1 = bufs[0][f"pre{i}"], bufs[1][f"pre{i}"]
+            post0, post1 = bufs[0][f"post{i}"], bufs[1][f"post{i}"]
+            assert np.array_equal(post0, post1), i
+            if seq[i][0] == "ar":
+                assert np.array_equal(post0, pre0 + pre1), i  # sum of the two ranks' local buffers
+                assert not np.array_equal(pre0, pre1)          # rank-distinct batches
+            else:
+                assert np.array_equal(post0, pre0), i          # rank 0's data everywhere
+
+
+def test_identity_collective_changes_nothing():
+    from burn_raymarching_amd import host as H
+    res_a, raw_a = H.train(_cfg(H, seed=5))
+    calls = []
+    comm = H.collective(0, 1, lambda b, c, s: calls.append(c), lambda b, c, r, s: calls.append(-c))
+    cfg = _cfg(H, seed=5)
+    cfg.comm = ctypes.pointer(comm)
+    res_b, raw_b = H.train(cfg)
+    assert np.array_equal(raw_a, raw_b) and res_a.num_spheres == res_b.num_spheres
+    assert len(calls) == STAGES * STEPS + 2 * (STAGES - 1)
+
+
+def test_cli_ranks_1_over_rccl(tmp_path):
+    exe = os.path.join(ROOT, "burn_raymarching_amd", "lib", "rm_train")
+    out = subprocess.run([exe, "train", "--ranks", "1", "--cameras", os.path.join(GOLDEN, "cameras.json"),
+                          "--out", str(tmp_path), "--stages", str(STAGES), "--steps", str(STEPS), "--batch",
+                          str(BATCH), "--log-every", "0", "--no-previews"], capture_output=True, text=True,
+                         timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["ranks"] == 1 and line["steps"] == STAGES * STEPS
+    assert os.path.exists(tmp_path / "scene.json")
