@@ -69,7 +69,8 @@ namespace rm {
 // kRender: the non-differentiable target renderer of renderer.rs:4-80 (generate.rs)
 enum Mode { kFwd = 0, kBwd = 1, kTrain = 2, kRender = 3 };
 
-constexpr int kMaxBlocksPerLaunch = 16384;  // bounds the partial-gradient workspace per launch (16 views of 512x512)
+// bounds the partial-gradient workspace per launch: 16 views of 512x512
+constexpr int kMaxBlocksPerLaunch = 16384 * (256 / kBlock);
 #ifndef RM_REDUCE_SEGS
 #define RM_REDUCE_SEGS 128
 #endif
@@ -1287,6 +1288,10 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     // Each remaining step is >= dist - R' long and keeps the ray receding, so the distance
     // grows step by step (write_bound): with n steps left the ray is gone once
     // (1 - 1e-5) dist >= T(n) -- proven long before the ray gets there.
+#ifdef RM_LANE_STATS  // measurement build: lane-steps of escaped (or invalid) rays in marching waves
+    unsigned long long lane_gone_steps = 0;
+    int lanes_gone_last = 0;
+#endif
     auto wave_escaped = [&](int st, const float p[3]) {
       if (!(a.gone_d > 0.0f)) return false;
       const float ex = p[0] - c0x, ey = p[1] - c0y, ez = p[2] - c0z;
@@ -1297,6 +1302,10 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
         steps_saved += a.steps - st;
         return true;
       }
+#ifdef RM_LANE_STATS
+      lane_gone_steps += __popcll(__ballot(gone || !valid));
+      lanes_gone_last = __popcll(__ballot(gone || !valid));
+#endif
       return false;
     };
     int st0 = 0;
@@ -1335,6 +1344,10 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
       lb = D - fabsf(D);
       Dprev = D;
     }
+#ifdef RM_LANE_STATS  // stats[3] += escaped lane-steps of the march + 5 sweeps per escaped lane of a live wave
+    if (a.stats != nullptr && lane == 0)
+      atomicAdd(a.stats + 3, lane_gone_steps + (dead ? 0ull : 5ull * (unsigned long long)lanes_gone_last));
+#endif
   }
 #if RM_PRIO_RAMP
   __builtin_amdgcn_s_setprio(1);
@@ -2267,14 +2280,20 @@ int fail(rm_context* ctx, int code, const char* fmt, ...) {
     if (e_ != hipSuccess) return fail(ctx, RM_ERR_HIP, "%s: %s", #call, hipGetErrorString(e_)); \
   } while (0)
 
-// Centre-out dispatch order of the tx x ty tiles of a view (ray_block): by distance of the
-// tile centre from the image centre, ties by tile index. Built once per image size.
+// Centre-out dispatch order of the ray blocks of a view's tx x ty 16x16 tiles (ray_block): by
+// distance of the block's pixel-centre from the image centre, ties by block index. A block is a
+// whole tile (256-ray blocks) or one of its four 8x8 quadrants (64-ray blocks, RM_BLOCK=64), in
+// the pixel order of setup_ray. Built once per image size.
 int ensure_block_order(rm_context* ctx, int tx, int ty) {
   if (ctx->block_order && ctx->order_tx == tx && ctx->order_ty == ty) return RM_OK;
-  std::vector<int> ord((size_t)tx * ty);
+  constexpr int sub = 256 / kBlock;  // blocks per 16x16 tile
+  static_assert(sub == 1 || sub == 4, "ray blocks are 16x16 tiles or their 8x8 quadrants");
+  std::vector<int> ord((size_t)tx * ty * sub);
   for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
-  auto key = [&](int i) {
-    const long long dx = 2LL * (i % tx) + 1 - tx, dy = 2LL * (i / tx) + 1 - ty;
+  auto key = [&](int i) {  // twice the pixel offset of the block centre from the image centre
+    const int tile = i / sub, q = i % sub;
+    const long long ox = sub == 1 ? 16 : 16 * (q & 1) + 8, oy = sub == 1 ? 16 : 16 * (q >> 1) + 8;
+    const long long dx = 32LL * (tile % tx) + ox - 16LL * tx, dy = 32LL * (tile / tx) + oy - 16LL * ty;
     return dx * dx + dy * dy;
   };
   std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return key(x) < key(y); });
@@ -2770,6 +2789,9 @@ int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset) {
   out->waves = ctx->stats_blocks * kWaves;
   out->waves_exited = (int64_t)v[1];
   out->steps_saved = (int64_t)v[2];
+#ifdef RM_LANE_STATS
+  std::fprintf(stderr, "RM_LANE_STATS escaped_lane_sweeps %llu\n", v[3]);
+#endif
   if (reset) {
     RM_HIP(ctx, hipMemsetAsync(ctx->stats_dev, 0, sizeof v, ctx->stream));
     ctx->stats_blocks = 0;

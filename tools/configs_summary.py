@@ -1,0 +1,53 @@
+"""Collect the per-config bench lines and rocprofv3 stats of tools/gpu_configs2.sh into one
+profiles/<tag>_configs.json: per config the bench numbers (value, ms per step, train-kernel time,
+executed and canonical roofline fractions) and, from the rocprofv3 --stats run of the same
+arguments, the average time per call of every kernel and the per-step time outside the train
+kernel.
+
+    python3 tools/configs_summary.py gpurun_out/configs_<tag> profiles/<tag>_configs.json
+"""
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def main():
+    src, out = sys.argv[1], sys.argv[2]
+    res = {}
+    for path in sorted(glob.glob(os.path.join(src, "*.json"))):
+        name = os.path.basename(path)[:-5]
+        try:
+            d = json.load(open(path))
+        except ValueError:
+            continue
+        r = d.get("roofline") or {}
+        entry = {"config": d["config"], "value": d["value"], "value_median": d.get("value_median"),
+                 "ms_per_step": d["ms_per_step"], "ms_per_step_median": d.get("ms_per_step_median"),
+                 "train_kernel_ms": r.get("kernel_ms_per_step"), "frac": r.get("frac"),
+                 "executed_frac": r.get("executed_frac"), "canonical_frac": (r.get("canonical") or {}).get("frac"),
+                 "finite": d.get("finite")}
+        stats = glob.glob(os.path.join(src, f"prof_{name}", "**", "*kernel_stats.csv"), recursive=True)
+        if stats:
+            rows = list(csv.DictReader(open(stats[0])))
+            kern = {}
+            for row in rows:
+                kern[row["Name"][:90]] = {"calls": int(row["Calls"]), "avg_us": round(float(row["AverageNs"]) / 1e3, 2)}
+            entry["rocprof_kernels"] = kern
+            train = next((v for k, v in kern.items() if "rm_ray_kernel<2, true>" in k), None)
+            if train:
+                entry["rocprof_train_avg_us"] = train["avg_us"]
+                steps = train["calls"]
+                other = sum(v["avg_us"] * v["calls"] for k, v in kern.items()
+                            if k.startswith("rm::") or "rm_optimizer" in k or "rm_ray_kernel<2" in k)
+                entry["rocprof_other_us_per_step"] = round((other - train["avg_us"] * steps) / steps, 2)
+        res[name] = entry
+    json.dump(res, open(out, "w"), indent=1)
+    for k, v in res.items():
+        print(k, v["value"], v["ms_per_step"], v.get("train_kernel_ms"), v.get("frac"), v.get("canonical_frac"),
+              v.get("rocprof_train_avg_us"), v.get("rocprof_other_us_per_step"))
+
+
+if __name__ == "__main__":
+    main()
