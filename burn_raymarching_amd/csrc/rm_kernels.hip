@@ -649,15 +649,11 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
     consume(D, w1);
     RM_SCHED_BARRIER();
   }
-  // partial sums of ray 16cb + n sit in the four lane groups: reduce across them, keep own ray
-  float own = 0.0f;
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb) {
-    float s = acc[cb];
-    s += __shfl_xor(s, 16);
-    s += __shfl_xor(s, 32);
-    if (cb == g) own = s;
-  }
+  // partial sums of ray 16cb + n sit in the four lane groups: one transposing reduction (two
+  // v_permlane32_swap and one v_permlane16_swap, no LDS) leaves lane (n, g) with the total of
+  // its own ray 16g + n: rows 0/2 keep the column blocks 0/2 summed over lane bit 5, rows 1/3
+  // the blocks 1/3, then each row adds its bit-4 partner
+  const float own = swap16_sum(swap32_sum(acc[0], acc[2]), swap32_sum(acc[1], acc[3]));
   __builtin_amdgcn_wave_barrier();  // the exchange is rewritten by the next step
   return own;
 }
