@@ -88,7 +88,8 @@ struct KArgs {
   float cull_min_d;  // scene distance at which the silhouette mask is exactly 0
   float lse_slack;  // ln(M) / k (rounded up): the hard min exceeds the soft-min by at most this
   unsigned long long* stats;  // nullable: [0] += 1 per escaped (skipped) block
-  float gone_d;               // > 0: waves whose rays all escaped past this distance stop marching
+  float gone_d;               // > 0: rays that provably escape past this distance are `gone` (see the march)
+  int early_exit;             // waves whose rays are all gone stop marching
   int mfma;                   // march sums on the matrix cores (lse_mfma) instead of lse_weighted
   int shift_max;              // RM_MARCH_FORCE_MAX_SHIFT: every march step takes the running-max shift
   const int* esc_flags;       // nullable: per-block escape flags of this launch (rm_escape_kernel)
@@ -127,7 +128,21 @@ struct KArgs {
   float* dbg;       // optional per-ray intermediates [n][16] (diagnostics; see rm_debug_intermediates)
   float* partials;  // [gridDim.x][rec], rec = Mpad*12 + 8
   long long rec;
+#ifdef RM_BLOCK_TRACE
+  unsigned long long* btrace;  // measurement build: per-wave timing records (rm_ray_kernel)
+#endif
 };
+#ifdef RM_BLOCK_TRACE
+constexpr int kTraceWords = 12;
+// measurement build: word w of this wave's record (lane 0 writes)
+__device__ __forceinline__ void trace_word(const KArgs& a, int w, unsigned long long v) {
+  if (a.btrace != nullptr && (threadIdx.x & 63) == 0)
+    a.btrace[kTraceWords * ((unsigned long long)blockIdx.x * kWaves + (threadIdx.x >> 6)) + w] = v;
+}
+#define RM_TRACE(w, v) trace_word(a, (w), (v))
+#else
+#define RM_TRACE(w, v) ((void)0)
+#endif
 
 // ---- sphere records: pair-interleaved, in global memory, read through scalar loads ----------
 // rm_prep_kernel writes them once per call. Pair i holds spheres (2i, 2i+1) so every sweep runs
@@ -205,9 +220,9 @@ constexpr size_t kSlotBytes0 = (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float
 constexpr size_t kSlotBytes = RM_BWD_TRANSPOSED && kSlotBwdT > kSlotBytes0 ? kSlotBwdT : kSlotBytes0;
 __host__ __device__ constexpr size_t lds_bytes() { return kSlotBytes + 256; }
 
-// three-value block reduction (min, max, max) for the record header
+// three-value block reduction (min, max, max) for the record header (blockDim.x / 64 <= 16 waves)
 __device__ __forceinline__ void header_reduce(float& rmin, float& rmax, float& spread, float* dst) {
-  __shared__ float red[3][4];
+  __shared__ float red[3][16];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
     rmin = fminf(rmin, __shfl_xor(rmin, off));
@@ -222,7 +237,7 @@ __device__ __forceinline__ void header_reduce(float& rmin, float& rmax, float& s
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w2 = 1; w2 < 4; ++w2) {
+    for (int w2 = 1; w2 < (int)(blockDim.x >> 6); ++w2) {
       red[0][0] = fminf(red[0][0], red[0][w2]);
       red[1][0] = fmaxf(red[1][0], red[1][w2]);
       red[2][0] = fmaxf(red[2][0], red[2][w2]);
@@ -235,11 +250,12 @@ __device__ __forceinline__ void header_reduce(float& rmin, float& rmax, float& s
 }
 
 // Bounding sphere of the scene, block-wide: c0 = centre of the centres' bounding box,
-// R >= |c_j - c0| + r_j for every sphere (rounded up). scratch: >= 8*kWaves floats of LDS.
+// R >= |c_j - c0| + r_j for every sphere (rounded up). scratch: >= 8 floats of LDS per wave of
+// the block.
 __device__ __forceinline__ void scene_bound(const KArgs& a, float* scratch, int tid, float c0[3], float& R) {
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = tid >> 6, nt = (int)blockDim.x, nw = nt >> 6;
   float v[6] = {INFINITY, INFINITY, INFINITY, -INFINITY, -INFINITY, -INFINITY};
-  for (int j = tid; j < a.M; j += kBlock)
+  for (int j = tid; j < a.M; j += nt)
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const float c = a.centers[3 * j + k];
@@ -260,14 +276,14 @@ __device__ __forceinline__ void scene_bound(const KArgs& a, float* scratch, int 
 #pragma unroll
   for (int k = 0; k < 3; ++k) {
     float lo = scratch[k], hi = scratch[3 + k];
-    for (int w = 1; w < kWaves; ++w) {
+    for (int w = 1; w < nw; ++w) {
       lo = fminf(lo, scratch[8 * w + k]);
       hi = fmaxf(hi, scratch[8 * w + 3 + k]);
     }
     c0[k] = 0.5f * (lo + hi);
   }
   float r = 0.0f;
-  for (int j = tid; j < a.M; j += kBlock) {
+  for (int j = tid; j < a.M; j += nt) {
     const float dx = a.centers[3 * j] - c0[0], dy = a.centers[3 * j + 1] - c0[1], dz = a.centers[3 * j + 2] - c0[2];
     r = fmaxf(r, fsqrt(dx * dx + dy * dy + dz * dz) + a.radius[j]);  // 1 ulp: inside the round-up below
   }
@@ -277,7 +293,7 @@ __device__ __forceinline__ void scene_bound(const KArgs& a, float* scratch, int 
   if (lane == 0) scratch[8 * wave] = r;
   __syncthreads();
   R = scratch[0];
-  for (int w = 1; w < kWaves; ++w) R = fmaxf(R, scratch[8 * w]);
+  for (int w = 1; w < nw; ++w) R = fmaxf(R, scratch[8 * w]);
   R = R * (1.0f + 1e-5f) + 1e-6f;  // cover the f32 rounding of |c - c0| + r
   __syncthreads();  // scratch is reused by the caller
 }
@@ -333,7 +349,7 @@ __device__ __forceinline__ uint4 mfma_a_frag(const KArgs& a, int rb, int l) {
 // (R' + sqrt(2 y^2 - R'^2)) / 2 with y = T(n - 1) / (1 - 1e-5), rounded up. For n >= kEscTab the
 // march uses T(kEscTab - 1) >= T(n).
 __device__ void write_bound(const KArgs& a, float* hdr, float* esc) {
-  __shared__ float scratch[8 * kWaves];
+  __shared__ float scratch[8 * 16];
   float c[3], R;
   scene_bound(a, scratch, threadIdx.x, c, R);
   if (threadIdx.x == 0) {
@@ -366,21 +382,22 @@ __device__ void write_bound(const KArgs& a, float* hdr, float* esc) {
 // rm_prep_finish); the final header also gets the scene's bounding sphere (scene_bound).
 constexpr int kPrepStageMax = 512;  // one-block prep: parameters staged in LDS up to this M
 
-__device__ void write_origins(const KArgs& a, const float4* rec, const uint4* At, const float* Wt, const float* hdr,
-                              float* orig, unsigned char* xch, int v);
+__device__ void write_origins(const KArgs& a, const float4& S00, const float4& S10, float rmax, float spread,
+                              const uint4* At, const float* Wt, float* orig, unsigned char* xch, int v);
 
 __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __restrict__ rec) {
   // One-block case: stage the parameters in LDS once (one load round instead of one per phase:
   // records, MFMA tiles, header, bounding sphere); the phases below read them through `a`.
   __shared__ float stage[7 * kPrepStageMax];
+  const int nt = (int)blockDim.x;
   KArgs a = a0;
   if (gridDim.x == 1 && a0.M <= kPrepStageMax) {
     const int M = a0.M;
-    for (int e = threadIdx.x; e < 3 * M; e += 256) {
+    for (int e = threadIdx.x; e < 3 * M; e += nt) {
       stage[e] = a0.centers[e];
       stage[3 * M + e] = a0.colors_h != nullptr ? (float)a0.colors_h[e] : a0.colors[e];
     }
-    for (int e = threadIdx.x; e < M; e += 256) stage[6 * M + e] = a0.radius[e];
+    for (int e = threadIdx.x; e < M; e += nt) stage[6 * M + e] = a0.radius[e];
     __syncthreads();
     a.centers = stage;
     a.colors = stage + 3 * M;
@@ -401,7 +418,7 @@ __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __
   const float kr_first = kappa * a.radius[0];
   const float c0x = a.centers[0], c0y = a.centers[1], c0z = a.centers[2];
   float rmin = INFINITY, rmax = 0.0f, spread = 0.0f;
-  const int ip = blockIdx.x * 256 + threadIdx.x;
+  const int ip = blockIdx.x * nt + threadIdx.x;
   if (ip < np) {
     float gx[2], gy[2], gz[2], cc[2], kr[2], rr[2], cr[2], cg[2], cb[2], w[2], wf[2];
 #pragma unroll
@@ -456,9 +473,9 @@ __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __
   uint4* At = reinterpret_cast<uint4*>(tiles);
   float* Wt = reinterpret_cast<float*>(At + (size_t)nrb * 64);
 #ifndef RM_DBG_NO_TILES
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < nrb * 64; e += gridDim.x * 256) At[e] = mfma_a_frag(a, e >> 6, e & 63);
+  for (int e = blockIdx.x * nt + threadIdx.x; e < nrb * 64; e += gridDim.x * nt) At[e] = mfma_a_frag(a, e >> 6, e & 63);
 #endif
-  for (int e = blockIdx.x * 256 + threadIdx.x; e < nrb * 32; e += gridDim.x * 256) {
+  for (int e = blockIdx.x * nt + threadIdx.x; e < nrb * 32; e += gridDim.x * nt) {
     const int j = 16 * (e >> 5) + (e & 15);
     const float krj = j < a.M ? kappa * a.radius[j] : 0.0f;
     Wt[e] = j >= a.M ? 0.0f : ((e & 16) ? fexp2(krj - kr_first) : fexp2(krj));
@@ -490,7 +507,7 @@ __global__ __launch_bounds__(64) void rm_origin_kernel(const KArgs a, const floa
   const uint4* At = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(rec) + tiles_offset(np, nprep));
   const float* Wt = reinterpret_cast<const float*>(At + (size_t)(np / 8) * 64);
   const float* hdr = reinterpret_cast<const float*>(reinterpret_cast<const float2*>(rec + 7 * (size_t)np) + np);
-  write_origins(a, rec, At, Wt, hdr, a.origin, xch, blockIdx.x);
+  write_origins(a, rec[4 * np], rec[5 * np], hdr[1], hdr[2], At, Wt, a.origin, xch, blockIdx.x);
 }
 
 // ---- packed helpers --------------------------------------------------------------------------
@@ -500,7 +517,13 @@ __device__ __forceinline__ f2 sqrt2(f2 q) { return f2{fsqrt(q.x), fsqrt(q.y)}; }
 __device__ __forceinline__ f2 exp2v(f2 x) { return f2{fexp2(x.x), fexp2(x.y)}; }
 __device__ __forceinline__ f2 rcp2(f2 x) { return f2{frcp(x.x), frcp(x.y)}; }
 __device__ __forceinline__ f2 rsq2(f2 x) { return f2{frsq(x.x), frsq(x.y)}; }
-__device__ __forceinline__ f2 clamp_q(f2 q) { return f2{fmaxf(q.x, 1e-6f), fmaxf(q.y, 1e-6f)}; }
+// max(q, qmin) for qmin > 0 as one integer max on the bit patterns (non-negative floats order
+// like their bits, negative ones have negative bit patterns): fmaxf in the kernels' IEEE mode
+// costs a canonicalising v_max before the v_max. Equal to fmaxf for every non-NaN q.
+__device__ __forceinline__ float qclamp(float q, float qmin) {
+  return __int_as_float(max(__float_as_int(q), __float_as_int(qmin)));
+}
+__device__ __forceinline__ f2 clamp_q(f2 q) { return f2{qclamp(q.x, 1e-6f), qclamp(q.y, 1e-6f)}; }
 __device__ __forceinline__ f2 lo(const float4& v) { return f2{v.x, v.y}; }
 __device__ __forceinline__ f2 hi(const float4& v) { return f2{v.z, v.w}; }
 
@@ -623,7 +646,7 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
       const float wv[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
-        if constexpr (CLAMP) q[v] = fmaxf(q[v], QMIN);
+        if constexpr (CLAMP) q[v] = qclamp(q[v], QMIN);
         const float rho = fsqrt(q[v]);
         acc[cb] = fmaf(wv[v], fexp2(FIXED ? S[cb] - rho : -rho), acc[cb]);
       }
@@ -674,7 +697,7 @@ __device__ __forceinline__ float march_d_none(const float p[3], float kappa, flo
 __device__ __forceinline__ float fixed_shift(const float p[3], float k2, const float4& S00, const float4& S10) {
 #pragma clang fp contract(off)
   const float q0 = fmaf(p[2], S10.x, fmaf(p[1], S00.z, fmaf(p[0], S00.x, fmaf(k2, psq(p), S10.z))));
-  return fsqrt(fmaxf(q0, k2 * 1e-6f));
+  return fsqrt(qclamp(q0, k2 * 1e-6f));
 }
 
 // A march step's soft-min D at p on the matrix cores with the fixed shift sh = rho'_0 (sphere 0;
@@ -701,12 +724,11 @@ __device__ __forceinline__ float march_d_fixed(const float p[3], float kappa, fl
 // (vector-only march, or the fixed shift not provably safe): those rays march it themselves.
 // rec / hdr: this call's complete records and header; At / Wt: its march tiles; xch: 64 x 36 B
 // of LDS. One wave computes view v.
-__device__ void write_origins(const KArgs& a, const float4* rec, const uint4* At, const float* Wt, const float* hdr,
-                              float* orig, unsigned char* xch, int v) {
+__device__ void write_origins(const KArgs& a, const float4& S00, const float4& S10, float rmax, float spread,
+                              const uint4* At, const float* Wt, float* orig, unsigned char* xch, int v) {
   const int lane = threadIdx.x & 63;
   const int np = a.Mpad / 2;
   const float kappa = a.k * kLog2e, inv_kappa = 1.0f / kappa;
-  const float rmax = hdr[1], spread = hdr[2];
   const bool shift_fixed_ok = kappa * (rmax + spread) * 1.001f <= 100.0f;
   const bool shift_none_ok = kappa * rmax * 1.001f <= 30.0f;
   const float kr_first = kappa * a.radius[0];
@@ -718,12 +740,11 @@ __device__ void write_origins(const KArgs& a, const float4* rec, const uint4* At
     float D = __builtin_nanf("");
     // the first step's choice in soft_min_march: unshifted when sphere 0 proves it safe, else
     // the fixed shift (else the vector path: not shared)
-    const bool none = a.mfma && shift_none_ok && fixed_shift(p, kappa * kappa, rec[4 * np], rec[5 * np]) - kr_first <= 90.0f;
+    const bool none = a.mfma && shift_none_ok && fixed_shift(p, kappa * kappa, S00, S10) - kr_first <= 90.0f;
     if (none)
       D = march_d_none<true>(p, kappa, inv_kappa, At, Wt, np / 8, xa, xb, xs, lane);
     else if (a.mfma && shift_fixed_ok && psq(p) <= 1e10f)
-      D = march_d_fixed<true>(p, kappa, inv_kappa, kr_first, rec[4 * np], rec[5 * np], At, Wt, np / 8, xa, xb, xs,
-                              lane);
+      D = march_d_fixed<true>(p, kappa, inv_kappa, kr_first, S00, S10, At, Wt, np / 8, xa, xb, xs, lane);
     if (lane == 0) orig[v] = D;
   }
 }
@@ -741,7 +762,7 @@ __device__ __forceinline__ float lse_weighted(const float p[3], const Lds& L, in
     for (int ii = 0; ii < 8; ++ii) {
       const float4 A = Lds::v4(L.S0[i0 + ii]), B = Lds::v4(L.S1[i0 + ii]), Wt = Lds::v4(L.W[i0 + ii]);
       f2 q = qpair(PX, PY, PZ, PP, A, B);
-      if constexpr (CLAMP) q = f2{fmaxf(q.x, QMIN.x), fmaxf(q.y, QMIN.y)};
+      if constexpr (CLAMP) q = f2{qclamp(q.x, QMIN.x), qclamp(q.y, QMIN.y)};
       const f2 rho = sqrt2(q);
       if constexpr (FIXED) {
         if (i0 == 0 && ii == 0) SH = sp(rho.x);
@@ -820,7 +841,7 @@ __device__ __forceinline__ void lse_taps_w(const float p[3], const Lds& L, int n
                  fma2(ez, NTE, Q)};
 #pragma unroll
       for (int t = 0; t < 6; ++t) {
-        if constexpr (CLAMP) q[t] = f2{fmaxf(q[t].x, QMIN.x), fmaxf(q[t].y, QMIN.y)};
+        if constexpr (CLAMP) q[t] = f2{qclamp(q[t].x, QMIN.x), qclamp(q[t].y, QMIN.y)};
         acc[t] = fma2(W, exp2v(-sqrt2(q[t])), acc[t]);
       }
     }
@@ -1126,7 +1147,34 @@ __global__ __launch_bounds__(kBlock) void rm_escape_kernel(const KArgs a, int* _
 }
 
 template <int MODE, bool CAM>
+__device__ __forceinline__ void ray_body(const KArgs& a);
+
+// The per-ray kernel. Measurement build (-DRM_BLOCK_TRACE): every wave also records {start, end}
+// (s_memrealtime, 100 MHz), its hardware slot (HW_ID | XCC_ID << 32), {logical block, launch
+// position}, the times its march and its post-march forward ended and its march steps saved into
+// a.btrace[kTraceWords * (blockIdx.x * kWaves + wave) ...] (tools/block_trace.py).
+template <int MODE, bool CAM>
 __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const KArgs a) {
+#ifdef RM_BLOCK_TRACE
+  const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
+  ray_body<MODE, CAM>(a);
+  const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
+  if (a.btrace != nullptr && (threadIdx.x & 63) == 0) {
+    const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
+    const unsigned xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20);  // HW_REG_XCC_ID
+    unsigned long long* r = a.btrace + kTraceWords * ((unsigned long long)blockIdx.x * kWaves + (threadIdx.x >> 6));
+    r[0] = t_begin;
+    r[1] = t_end;
+    r[2] = (unsigned long long)hw | ((unsigned long long)xcc << 32);
+    r[3] = (unsigned long long)ray_block(a) | ((unsigned long long)blockIdx.x << 32);
+  }
+#else
+  ray_body<MODE, CAM>(a);
+#endif
+}
+
+template <int MODE, bool CAM>
+__device__ __forceinline__ void ray_body(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   Lds L;
   {
@@ -1183,7 +1231,10 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   const bool shift_none_ok = !a.shift_max && kappa * rmax * 1.001f <= 30.0f;
   const float kr_first = kappa * a.radius[0];
   // Wave-uniform choice of the clamp-free path from a per-lane lower bound on the distance.
-  auto all_safe = [&](float dist_lb) { return __all(dist_lb + rmin >= kSafeRho) != 0; };
+  // Rays proven to escape (`gone`, see the march) no longer take part in the wave-uniform
+  // choices: their outputs and gradient terms are exactly 0 whatever they compute.
+  bool gone = false;
+  auto all_safe = [&](float dist_lb) { return __all(dist_lb + rmin >= kSafeRho || gone) != 0; };
 
   // every sweep visits all sphere pairs in one pass (records are not staged)
   auto for_tiles = [&](auto&& body) { body(0, a.Mpad); };
@@ -1200,29 +1251,47 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
   // The march's soft-min with the cheapest safe shift (the result differs only by fp32 rounding).
   // kShiftNone needs the hard maximum -kappa d_min >= -100 at the new point: d_min(new) <=
   // d_min(old) + |D| <= D + ln(M)/k + |D| (the soft-min is within ln(M)/k below the hard min).
+#ifdef RM_BLOCK_TRACE
+  // measurement build: march steps per path (16 bits each: none fast, none clamped, fixed fast,
+  // fixed clamped), shader cycles inside the matrix-core steps, vector-path steps
+  unsigned long long tr_paths = 0, tr_lse_cyc = 0, tr_vec = 0;
+#endif
   auto soft_min_march = [&](const float p[3], bool fast, float Dprev) {
-    bool none = shift_none_ok && __all(2.0f * fmaxf(Dprev, 0.0f) + a.lse_slack <= 90.0f * inv_kappa);
+    bool none = shift_none_ok && __all(2.0f * fmaxf(Dprev, 0.0f) + a.lse_slack <= 90.0f * inv_kappa || gone);
     // or: the nearest sphere is no farther than sphere 0, k (rho_0 - r_0) = rho'_0 - k r_0 <= 90
     // bounds k d_min just as well (the first steps after the eye, where the 2 D bound is loose)
     if (!none && shift_none_ok && a.mfma)
-      none = __all(fixed_shift(p, kappa * kappa, Lds::v4(L.S0[0]), Lds::v4(L.S1[0])) - kr_first <= 90.0f);
+      none = __all(fixed_shift(p, kappa * kappa, Lds::v4(L.S0[0]), Lds::v4(L.S1[0])) - kr_first <= 90.0f || gone);
     float m = none ? 0.0f : -INFINITY, s = 0.0f;
-    const bool fixed = !none && shift_fixed_ok && __all(psq(p) <= 1e10f);
+    const bool fixed = !none && shift_fixed_ok && __all(psq(p) <= 1e10f || gone);
     if ((none || fixed) && a.mfma) {
       const float k2 = kappa * kappa;
       const int nrb = a.Mpad / 16;
       uint4* xa = reinterpret_cast<uint4*>(L.slots) + wave * 64;
       uint4* xb = reinterpret_cast<uint4*>(L.slots) + kWaves * 64 + wave * 64;
       float* xs = L.slots + kWaves * 64 * 8 + wave * 64;
+#ifdef RM_BLOCK_TRACE
+      const unsigned long long tq0 = __builtin_readcyclecounter();
+      tr_paths += 1ull << (16 * ((fixed ? 2 : 0) + (fast ? 0 : 1)));
+#endif
+      float Dm;
       if (fixed) {  // the ray's shift: rho'_0 of sphere 0 (any value near it keeps +-100 headroom)
         const float4 A = Lds::v4(L.S0[0]), B = Lds::v4(L.S1[0]);
-        return fast ? march_d_fixed<false>(p, kappa, inv_kappa, kr_first, A, B, L.At, L.Wt, nrb, xa, xb, xs, lane)
-                    : march_d_fixed<true>(p, kappa, inv_kappa, kr_first, A, B, L.At, L.Wt, nrb, xa, xb, xs, lane);
+        Dm = fast ? march_d_fixed<false>(p, kappa, inv_kappa, kr_first, A, B, L.At, L.Wt, nrb, xa, xb, xs, lane)
+                  : march_d_fixed<true>(p, kappa, inv_kappa, kr_first, A, B, L.At, L.Wt, nrb, xa, xb, xs, lane);
+      } else {
+        Dm = fast ? march_d_none<false>(p, kappa, inv_kappa, L.At, L.Wt, nrb, xa, xb, xs, lane)
+                  : march_d_none<true>(p, kappa, inv_kappa, L.At, L.Wt, nrb, xa, xb, xs, lane);
       }
       (void)k2;
-      return fast ? march_d_none<false>(p, kappa, inv_kappa, L.At, L.Wt, nrb, xa, xb, xs, lane)
-                  : march_d_none<true>(p, kappa, inv_kappa, L.At, L.Wt, nrb, xa, xb, xs, lane);
+#ifdef RM_BLOCK_TRACE
+      tr_lse_cyc += __builtin_readcyclecounter() - tq0;
+#endif
+      return Dm;
     }
+#ifdef RM_BLOCK_TRACE
+    ++tr_vec;
+#endif
     if (none || fixed) {
       const float k2 = kappa * kappa;
       const int np = a.Mpad / 2;
@@ -1279,22 +1348,30 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     // receding ray, so t keeps increasing); the reconnected point and the mask argument
     // are then >= gone_d too, where sigmoid(-msharp D) (or exp(-10 D^2)) is exactly 0 in
     // fp32: out = 0 and every gradient term is 0, whatever the remaining steps would give.
-    // A wave whose rays have all escaped stops here. Margins: 1e-5 relative + 1e-3 cover
-    // the fp32 rounding of the march at any |p|.
+    // Margins: 1e-5 relative + 1e-3 cover the fp32 rounding of the march at any |p|.
     // Each remaining step is >= dist - R' long and keeps the ray receding, so the distance
     // grows step by step (write_bound): with n steps left the ray is gone once
     // (1 - 1e-5) dist >= T(n) -- proven long before the ray gets there.
+    // A gone ray (sticky) steps by that bound, dist - R', instead of its soft-min: the proof
+    // holds for any steps >= the bound, so its outputs stay exactly 0, and it leaves the
+    // wave's shift / clamp choices (far points would force the running-max vector sweep on
+    // the whole wave: 48 % of the march steps at 4096 spheres / 128 steps). A wave whose
+    // rays are all gone stops (a.early_exit). The same in every mode that builds the table,
+    // exit on or off, so both give the same bits.
+    const float rprime = (hdr[7] + a.lse_slack + 1e-3f) * (1.0f + 1e-6f);  // R' as in write_bound
 #ifdef RM_LANE_STATS  // measurement build: lane-steps of escaped (or invalid) rays in marching waves
     unsigned long long lane_gone_steps = 0;
     int lanes_gone_last = 0;
 #endif
+    float gone_step = 0.0f;  // dist - R' of a gone ray at the current point
     auto wave_escaped = [&](int st, const float p[3]) {
       if (!(a.gone_d > 0.0f)) return false;
       const float ex = p[0] - c0x, ey = p[1] - c0y, ez = p[2] - c0z;
       const float Tn = esc_tab[min(a.steps - st, kEscTab - 1)];
-      const bool gone = fmaf(ez, d[2], fmaf(ey, d[1], ex * d[0])) >= 0.0f &&
-                        fsqrt(fmaf(ez, ez, fmaf(ey, ey, ex * ex))) * (1.0f - 1e-5f) >= Tn;
-      if (__all(gone || !valid)) {
+      const float dist = fsqrt(fmaf(ez, ez, fmaf(ey, ey, ex * ex)));
+      gone = gone || (fmaf(ez, d[2], fmaf(ey, d[1], ex * d[0])) >= 0.0f && dist * (1.0f - 1e-5f) >= Tn);
+      gone_step = dist - rprime;
+      if (a.early_exit && __all(gone || !valid)) {
         steps_saved += a.steps - st;
         return true;
       }
@@ -1305,6 +1382,9 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
       return false;
     };
     int st0 = 0;
+#ifdef RM_BLOCK_TRACE
+    const unsigned long long tr_c_begin = __builtin_readcyclecounter();
+#endif
     if constexpr (CAM) {
       // Camera mode: step 0 from the soft-min at the eye, evaluated once per view by the same
       // code path (write_origins), when every lane of the wave has it (not NaN). Taken before
@@ -1316,7 +1396,7 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
           if (wave_escaped(0, p)) {
             dead = true;
           } else {  // == soft_min_march(p, all_safe(-inf) = false, inf) at p = o = the eye
-            t = fminf(t + D0, kTMax);
+            t = fminf(t + (gone ? gone_step : D0), kTMax);
             lb = D0 - fabsf(D0);
             Dprev = D0;
             st0 = 1;
@@ -1335,11 +1415,19 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
         break;
       }
       const float D = soft_min_march(p, all_safe(lb), Dprev);
-      t = fminf(t + D, kTMax);
+      t = fminf(t + (gone ? gone_step : D), kTMax);
       // next point: hard min >= soft-min D here, moved by |D|
       lb = D - fabsf(D);
       Dprev = D;
     }
+  RM_TRACE(4, __builtin_amdgcn_s_memrealtime());
+  RM_TRACE(6, (unsigned long long)steps_saved);
+#ifdef RM_BLOCK_TRACE
+  RM_TRACE(7, tr_paths);
+  RM_TRACE(8, tr_lse_cyc);
+  RM_TRACE(9, tr_vec);
+  RM_TRACE(10, __builtin_readcyclecounter() - tr_c_begin);
+#endif
 #ifdef RM_LANE_STATS  // stats[3] += escaped lane-steps of the march + 5 sweeps per escaped lane of a live wave
     if (a.stats != nullptr && lane == 0)
       atomicAdd(a.stats + 3, lane_gone_steps + (dead ? 0ull : 5ull * (unsigned long long)lanes_gone_last));
@@ -1484,6 +1572,7 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     a.out[3 * ri + 1] = outv[1];
     a.out[3 * ri + 2] = outv[2];
   }
+  RM_TRACE(5, __builtin_amdgcn_s_memrealtime());
   if constexpr (MODE == kFwd || MODE == kRender) return;
 #if RM_PRIO_RAMP
   __builtin_amdgcn_s_setprio(0);
@@ -2102,26 +2191,15 @@ __device__ __forceinline__ void block_sum4(float (&v)[4], float* red) {
   for (int c = 0; c < 4; ++c) v[c] = red[c * 256];
 }
 
-// Pass A of the optimizer: block s owns sphere s. It snapshots the sphere's raw parameters
-// (the update kernel reads neighbours' pre-step values) and, with penalties, sums the
-// repulsion row of training.rs:73-82 over j: dist_ij = sqrt(max(|c_i|^2 + |c_j|^2 - 2 c_i.c_j,
-// 1e-6)), value (dist + 100 I + 1e-6)^-1, gradient through both (s, j) and (j, s) entries.
-__global__ __launch_bounds__(256) void rm_penalty_pairs(const float* __restrict__ raw, int M, int with_pen,
-                                                        float* __restrict__ snap, float* __restrict__ pair) {
-  __shared__ float red[4 * 256];
-  const int s = blockIdx.x;
-  if (threadIdx.x < 7) {
-    const int idx = threadIdx.x < 3 ? 3 * s + threadIdx.x
-                                    : (threadIdx.x < 6 ? 3 * M + 3 * s + (threadIdx.x - 3) : 6 * M + s);
-    snap[idx] = raw[idx];
-  }
-  if (s == 0 && threadIdx.x >= 32 && threadIdx.x < 36) snap[7 * M + threadIdx.x - 32] = raw[7 * M + threadIdx.x - 32];
-  if (!with_pen) return;
-  const float cx = raw[3 * s], cy = raw[3 * s + 1], cz = raw[3 * s + 2];
+// Repulsion row of sphere s (training.rs:73-82) over j = j0, j0 + stride, ... < M, added to v:
+// dist_sj = sqrt(max(|c_s|^2 + |c_j|^2 - 2 c_s.c_j, 1e-6)), value (dist + 100 I + 1e-6)^-1 into
+// v[3], its gradient w.r.t. c_s through both the (s, j) and (j, s) entries into v[0..2].
+// c: the pre-step centres [M][3] (raw = activated).
+__device__ __forceinline__ void repulsion_row(const float* c, int M, int s, int j0, int stride, float (&v)[4]) {
+  const float cx = c[3 * s], cy = c[3 * s + 1], cz = c[3 * s + 2];
   const float csq = cx * cx + cy * cy + cz * cz;
-  float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (int j = threadIdx.x; j < M; j += 256) {
-    const float ox = raw[3 * j], oy = raw[3 * j + 1], oz = raw[3 * j + 2];
+  for (int j = j0; j < M; j += stride) {
+    const float ox = c[3 * j], oy = c[3 * j + 1], oz = c[3 * j + 2];
     const float q = (csq + (ox * ox + oy * oy + oz * oz)) - (cx * ox + cy * oy + cz * oz) * 2.0f;
     const float rho = sqrtf(fmaxf(q, 1e-6f));
     const float den = rho + (j == s ? 100.0f : 0.0f) + 1e-6f;
@@ -2133,13 +2211,101 @@ __global__ __launch_bounds__(256) void rm_penalty_pairs(const float* __restrict_
       v[2] += gs * (cz - oz);
     }
   }
+}
+
+// Pass A of the optimizer: block s owns sphere s. It snapshots the sphere's raw parameters
+// (the update kernel reads neighbours' pre-step values) and, with penalties, sums the
+// repulsion row of training.rs:73-82 over j (repulsion_row), block tree reduction.
+__global__ __launch_bounds__(256) void rm_penalty_pairs(const float* __restrict__ raw, int M, int with_pen,
+                                                        float* __restrict__ snap, float* __restrict__ pair) {
+  __shared__ float red[4 * 256];
+  const int s = blockIdx.x;
+  if (threadIdx.x < 7) {
+    const int idx = threadIdx.x < 3 ? 3 * s + threadIdx.x
+                                    : (threadIdx.x < 6 ? 3 * M + 3 * s + (threadIdx.x - 3) : 6 * M + s);
+    snap[idx] = raw[idx];
+  }
+  if (s == 0 && threadIdx.x >= 32 && threadIdx.x < 36) snap[7 * M + threadIdx.x - 32] = raw[7 * M + threadIdx.x - 32];
+  if (!with_pen) return;
+  float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  repulsion_row(raw, M, s, threadIdx.x, 256, v);
   block_sum4(v, red);
   if (threadIdx.x < 4) pair[4 * s + threadIdx.x] = v[threadIdx.x];
 }
 
-// Pass B: one thread per parameter element: chain rule of the activations, the compute_loss
-// penalties (training.rs:38-82), coupled weight decay and Burn's Adam; optionally writes the
-// activated parameters of the updated model (scene.rs:41-45) for the next step's render.
+// One parameter element i of the packed layout: chain rule of the activations, the compute_loss
+// penalties (training.rs:38-82), coupled weight decay and Burn's Adam; optionally the activated
+// parameters of the updated model (scene.rs:41-45) for the next step's render. raw: the pre-step
+// parameters (a snapshot: neighbours are read); pair: the repulsion rows. Returns the element's
+// penalty-loss share.
+__device__ __forceinline__ float optimizer_elem(int i, const float* raw, float* __restrict__ raw_out,
+                                                const float* __restrict__ gact, float* __restrict__ m1,
+                                                float* __restrict__ m2, const float* pair, int M, int step, float lr,
+                                                float wd, int with_pen, float* __restrict__ act_out,
+                                                _Float16* __restrict__ col_h_out) {
+  float pen = 0.0f;
+  const float x = raw[i];
+  float gv = gact[i];
+  const float invM = 1.0f / (float)M;
+  const float rep_scale = 1e-5f / ((float)M * (float)M);
+  if (i < 3 * M) {  // centers (identity activation)
+    if (with_pen) {
+      const int s = i / 3, ax = i - 3 * s;
+      const float cx = raw[3 * s], cy = raw[3 * s + 1], cz = raw[3 * s + 2];
+      const float rs = softplusf_(raw[6 * M + s]);  // penalties use softplus without +0.01 (training.rs:41)
+      gv += 0.05f * 2.0f * x / (3.0f * M);          // [b] mean(c^2) over [M,3] * 0.05
+      const float csq = cx * cx + cy * cy + cz * cz;
+      const float dist = sqrtf(csq + 1e-6f);
+      const float reach = dist + rs;                // [c] mean(mask * (|c| + r - 1.2)^2) * 5
+      if (reach > 1.2f) gv += 5.0f * invM * 2.0f * (reach - 1.2f) * (x / dist);
+      gv += rep_scale * pair[4 * s + ax];           // [d] repulsion (repulsion_row)
+      if (ax == 0) {
+        pen += 0.05f * csq / (3.0f * M);
+        if (reach > 1.2f) pen += 5.0f * invM * (reach - 1.2f) * (reach - 1.2f);
+        pen += rep_scale * pair[4 * s + 3];
+      }
+    }
+  } else if (i < 6 * M) {  // colors: d sigmoid = c (1 - c)
+    const float c = sigmoidf_(x);
+    gv *= c * (1.0f - c);
+  } else if (i < 7 * M) {  // radius: d (softplus + 0.01) = sigmoid
+    const float sg = sigmoidf_(x);
+    gv *= sg;
+    if (with_pen) {
+      const int s = i - 6 * M;
+      const float rs = softplusf_(x);
+      gv += 0.002f * invM * (rs > 0.0f ? 1.0f : (rs < 0.0f ? -1.0f : 0.0f)) * sg;  // [a] L1
+      pen += 0.002f * invM * fabsf(rs);
+      if (rs > 1.0f) {  // [a] large radius
+        gv += 0.04f * invM * 2.0f * rs * sg;
+        pen += 0.04f * invM * rs * rs;
+      }
+      const float cx = raw[3 * s], cy = raw[3 * s + 1], cz = raw[3 * s + 2];
+      const float reach = sqrtf(cx * cx + cy * cy + cz * cz + 1e-6f) + rs;
+      if (reach > 1.2f) gv += 5.0f * invM * 2.0f * (reach - 1.2f) * sg;  // [c] w.r.t. radius
+    }
+  } else if (i >= 7 * M + 3) {  // ambient: d sigmoid (light_dir raw: identity)
+    const float a = sigmoidf_(x);
+    gv *= a * (1.0f - a);
+  }
+  // Burn Adam with coupled weight decay: g += wd * theta; moments; bias correction.
+  gv = fmaf(wd, x, gv);
+  const float b1 = 0.9f, b2 = 0.999f, eps = 1e-5f;
+  const float mm = fmaf(b1, m1[i], (1.0f - b1) * gv);
+  const float vv = fmaf(b2, m2[i], (1.0f - b2) * gv * gv);
+  m1[i] = mm;
+  m2[i] = vv;
+  const float mh = mm / (1.0f - powf(b1, (float)step));
+  const float vh = vv / (1.0f - powf(b2, (float)step));
+  const float xn = x - lr * (mh / (sqrtf(vh) + eps));
+  raw_out[i] = xn;
+  if (act_out) act_out[i] = activate_elem(xn, i, M);
+  // fp16 colour models (RM_MARCH_COLOR_F16): the next render's colours, rounded to nearest
+  if (col_h_out != nullptr && i >= 3 * M && i < 6 * M) col_h_out[i - 3 * M] = (_Float16)activate_elem(xn, i, M);
+  return pen;
+}
+
+// Pass B: one thread per parameter element (optimizer_elem); per-block penalty partials.
 __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restrict__ raw, float* __restrict__ raw_out,
                                                            const float* __restrict__ gact,
                                                            float* __restrict__ m1, float* __restrict__ m2,
@@ -2152,66 +2318,7 @@ __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restri
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int n = 7 * M + 4;
   float pen = 0.0f;
-  if (i < n) {
-    const float x = raw[i];
-    float gv = gact[i];
-    const float invM = 1.0f / (float)M;
-    const float rep_scale = 1e-5f / ((float)M * (float)M);
-    if (i < 3 * M) {  // centers (identity activation)
-      if (with_pen) {
-        const int s = i / 3, ax = i - 3 * s;
-        const float cx = raw[3 * s], cy = raw[3 * s + 1], cz = raw[3 * s + 2];
-        const float rs = softplusf_(raw[6 * M + s]);  // penalties use softplus without +0.01 (training.rs:41)
-        gv += 0.05f * 2.0f * x / (3.0f * M);          // [b] mean(c^2) over [M,3] * 0.05
-        const float csq = cx * cx + cy * cy + cz * cz;
-        const float dist = sqrtf(csq + 1e-6f);
-        const float reach = dist + rs;                // [c] mean(mask * (|c| + r - 1.2)^2) * 5
-        if (reach > 1.2f) gv += 5.0f * invM * 2.0f * (reach - 1.2f) * (x / dist);
-        gv += rep_scale * pair[4 * s + ax];           // [d] repulsion (rm_penalty_pairs)
-        if (ax == 0) {
-          pen += 0.05f * csq / (3.0f * M);
-          if (reach > 1.2f) pen += 5.0f * invM * (reach - 1.2f) * (reach - 1.2f);
-          pen += rep_scale * pair[4 * s + 3];
-        }
-      }
-    } else if (i < 6 * M) {  // colors: d sigmoid = c (1 - c)
-      const float c = sigmoidf_(x);
-      gv *= c * (1.0f - c);
-    } else if (i < 7 * M) {  // radius: d (softplus + 0.01) = sigmoid
-      const float sg = sigmoidf_(x);
-      gv *= sg;
-      if (with_pen) {
-        const int s = i - 6 * M;
-        const float rs = softplusf_(x);
-        gv += 0.002f * invM * (rs > 0.0f ? 1.0f : (rs < 0.0f ? -1.0f : 0.0f)) * sg;  // [a] L1
-        pen += 0.002f * invM * fabsf(rs);
-        if (rs > 1.0f) {  // [a] large radius
-          gv += 0.04f * invM * 2.0f * rs * sg;
-          pen += 0.04f * invM * rs * rs;
-        }
-        const float cx = raw[3 * s], cy = raw[3 * s + 1], cz = raw[3 * s + 2];
-        const float reach = sqrtf(cx * cx + cy * cy + cz * cz + 1e-6f) + rs;
-        if (reach > 1.2f) gv += 5.0f * invM * 2.0f * (reach - 1.2f) * sg;  // [c] w.r.t. radius
-      }
-    } else if (i >= 7 * M + 3) {  // ambient: d sigmoid (light_dir raw: identity)
-      const float a = sigmoidf_(x);
-      gv *= a * (1.0f - a);
-    }
-    // Burn Adam with coupled weight decay: g += wd * theta; moments; bias correction.
-    gv = fmaf(wd, x, gv);
-    const float b1 = 0.9f, b2 = 0.999f, eps = 1e-5f;
-    const float mm = fmaf(b1, m1[i], (1.0f - b1) * gv);
-    const float vv = fmaf(b2, m2[i], (1.0f - b2) * gv * gv);
-    m1[i] = mm;
-    m2[i] = vv;
-    const float mh = mm / (1.0f - powf(b1, (float)step));
-    const float vh = vv / (1.0f - powf(b2, (float)step));
-    const float xn = x - lr * (mh / (sqrtf(vh) + eps));
-    raw_out[i] = xn;
-    if (act_out) act_out[i] = activate_elem(xn, i, M);
-    // fp16 colour models (RM_MARCH_COLOR_F16): the next render's colours, rounded to nearest
-    if (col_h_out != nullptr && i >= 3 * M && i < 6 * M) col_h_out[i - 3 * M] = (_Float16)activate_elem(xn, i, M);
-  }
+  if (i < n) pen = optimizer_elem(i, raw, raw_out, gact, m1, m2, pair, M, step, lr, wd, with_pen, act_out, col_h_out);
   if (pen_parts != nullptr) {
     float v[4] = {pen, 0.0f, 0.0f, 0.0f};
     block_sum4(v, red);
@@ -2253,6 +2360,10 @@ struct rm_context {
   int oturn = 0;                            // the list set the next keyed launch appends to
   unsigned long long cost_key = 0;          // geometry of the last keyed launch (its lists order the next)
   bool cost_valid = false;
+#ifdef RM_BLOCK_TRACE
+  unsigned long long* btrace = nullptr;     // measurement build: per-wave records of the last launch
+  long long btrace_waves = 0;
+#endif
 };
 
 namespace {
@@ -2518,11 +2629,14 @@ int run(rm_context* ctx, const Call& c) {
   // Escaped-ray early exit: the mask must be exactly 0 at distance gone_d -- exp2 of
   // msharp log2(e) D overflows at 128 (use 130; the reference's sigmoid(-15 D) is 0 from 5.92);
   // exp(-10 D^2) underflows long before 6.
+  // Gone rays (the march) in every mode but the diagnostics; the exit itself not when the march t
+  // of every ray is requested (t_out) or with RM_MARCH_NO_EARLY_EXIT.
   a.gone_d = 0.0f;
-  if ((c.march->flags & RM_MARCH_NO_EARLY_EXIT) == 0 && !c.t_out && !c.dbg) {
+  if (!c.dbg) {
     if (c.mode == kRender) a.gone_d = 6.0f;
     else if (a.msharp > 0.0f) a.gone_d = std::max(6.0f, 130.0f / (a.msharp * 1.44269504f));
   }
+  a.early_exit = a.gone_d > 0.0f && (c.march->flags & RM_MARCH_NO_EARLY_EXIT) == 0 && !c.t_out ? 1 : 0;
   if ((c.march->flags & RM_MARCH_ROW_ORDER) != 0) a.tiling = 0;
   a.mfma = (c.march->flags & RM_MARCH_VALU_ONLY) == 0;
   a.shift_max = (c.march->flags & RM_MARCH_FORCE_MAX_SHIFT) != 0;
@@ -2656,6 +2770,12 @@ int run(rm_context* ctx, const Call& c) {
         ++ctx->events_used;
       }
       dim3 grid((unsigned)nb);
+#ifdef RM_BLOCK_TRACE
+      if (!ctx->btrace)
+        RM_HIP(ctx, hipMalloc(&ctx->btrace, sizeof(unsigned long long) * kTraceWords * kWaves * (size_t)kMaxBlocksPerLaunch));
+      a.btrace = ctx->btrace;
+      ctx->btrace_waves = nb * kWaves;
+#endif
       if (c.mode == kFwd) launch_ray<kFwd>(c.cam, grid, lds, ctx->stream, a, ev0, ev1);
       else if (c.mode == kBwd) launch_ray<kBwd>(c.cam, grid, lds, ctx->stream, a, ev0, ev1);
       else if (c.mode == kTrain) launch_ray<kTrain>(c.cam, grid, lds, ctx->stream, a, ev0, ev1);
@@ -2759,6 +2879,19 @@ int rm_debug_order_counts(rm_context* ctx, int32_t* counts, int32_t capacity, in
   RM_HIP(ctx, hipMemcpy(counts, ctx->ocnt, sizeof(int) * 3 * kCls, hipMemcpyDeviceToHost));
   return RM_OK;
 }
+
+#ifdef RM_BLOCK_TRACE
+// Measurement build only (not in include/raymarch.h): the per-wave records of the last per-ray
+// launch, 4 x u64 per wave in launch order (see rm_ray_kernel). Synchronises the stream.
+int rm_debug_block_trace(rm_context* ctx, unsigned long long* host, int64_t cap_waves, int64_t* n_waves) {
+  if (!ctx || !host || !n_waves) return RM_ERR_INVALID_ARG;
+  RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  const long long n = std::min<long long>(ctx->btrace_waves, cap_waves);
+  *n_waves = n;
+  if (n > 0) RM_HIP(ctx, hipMemcpy(host, ctx->btrace, sizeof(unsigned long long) * kTraceWords * n, hipMemcpyDeviceToHost));
+  return RM_OK;
+}
+#endif
 
 int rm_stats_enable(rm_context* ctx, int32_t enable) {
   if (!ctx) return RM_ERR_INVALID_ARG;

@@ -84,3 +84,26 @@ def test_stats_count_shared_steps(mods, monkeypatch):
     assert s0["waves_exited"] == s1["waves_exited"]
     # every wave that did not leave at step 0 takes its first step from the shared value
     assert s0["steps_saved"] < s1["steps_saved"] <= s0["steps_saved"] + s1["waves"]
+
+
+@pytest.mark.parametrize("views,m", [(16, 256), (5, 512), (1, 8)])
+def test_origins_up_to_16_views(mods, monkeypatch, views, m):
+    """Per-view origin steps for up to 16 views per call (one wave per view in rm_origin_kernel):
+    images, loss and gradients equal (==) to the per-ray first step."""
+    torch, model, native, render = mods
+    sc = model.scene_tensors(model.synthetic_scene(m, 6), "cuda")
+    cams = model.ring_cameras(16)[:views]
+    tgt = render.render_diff_camera(cams, 32, 32, model.scene_tensors(model.synthetic_scene(m, 9), "cuda"), 32.0, 24)
+
+    def run():
+        out = torch.empty_like(tgt)
+        loss, g, _ = render.train_step_camera(cams, 32, 32, tgt, sc, 32.0, 0.3, 24, out=out,
+                                              march=native.march_params(24, 32.0))
+        torch.cuda.synchronize()
+        return loss.clone(), {key: v.clone() for key, v in g.items()}, out
+
+    per_ray, shared = _both(monkeypatch, run)
+    assert torch.equal(shared[0], per_ray[0])
+    assert torch.equal(shared[2], per_ray[2])
+    for key in shared[1]:
+        assert torch.equal(shared[1][key], per_ray[1][key]), key
