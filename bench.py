@@ -282,7 +282,8 @@ def main():
             replay(lambda j: ctx.timing(j % every == 0 and j > 0))
             ctx.timing(False)
             cms, cl = ctx.collect_timing(reset=True)
-            canon_ms = cms / cl if cl else None
+            canon_steps = sum(1 for j in range(args.steps) if j % every == 0 and j > 0)
+            canon_ms = cms / canon_steps if cl and canon_steps else None  # per step (a step may be several launches)
             march.flags &= ~native.RM_MARCH_NO_EARLY_EXIT
 
     if dist is not None:

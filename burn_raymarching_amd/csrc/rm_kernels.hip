@@ -71,6 +71,10 @@ enum Mode { kFwd = 0, kBwd = 1, kTrain = 2, kRender = 3 };
 
 // bounds the partial-gradient workspace per launch: 16 views of 512x512
 constexpr int kMaxBlocksPerLaunch = 16384 * (256 / kBlock);
+// automatic split march (RM_MARCH_SPLIT): from this many spheres, for launches of at most this
+// many rays (about one fill of the GPU: 1024 resident 256-ray blocks)
+constexpr int kSplitMinSpheres = 2048;
+constexpr long long kSplitMaxRays = 262144;
 #ifndef RM_REDUCE_SEGS
 #define RM_REDUCE_SEGS 128
 #endif
@@ -90,6 +94,7 @@ struct KArgs {
   unsigned long long* stats;  // nullable: [0] += 1 per escaped (skipped) block
   float gone_d;               // > 0: rays that provably escape past this distance are `gone` (see the march)
   int early_exit;             // waves whose rays are all gone stop marching
+  int split;                  // split march (RM_MARCH_SPLIT): 64 rays per block, a quarter of the spheres per wave
   int mfma;                   // march sums on the matrix cores (lse_mfma) instead of lse_weighted
   int shift_max;              // RM_MARCH_FORCE_MAX_SHIFT: every march step takes the running-max shift
   const int* esc_flags;       // nullable: per-block escape flags of this launch (rm_escape_kernel)
@@ -219,6 +224,9 @@ constexpr size_t kSlotBytes0 = (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float
                                    : (size_t)kWaves * 64 * 36;
 constexpr size_t kSlotBytes = RM_BWD_TRANSPOSED && kSlotBwdT > kSlotBytes0 ? kSlotBwdT : kSlotBytes0;
 __host__ __device__ constexpr size_t lds_bytes() { return kSlotBytes + 256; }
+// the split march's two combine buffers (kWaves x 64 floats each) after the march exchange
+constexpr int kSplitCombOff = kWaves * 64 * 9;  // floats: xa, xb (64 uint4 per wave each), xs
+static_assert((kSplitCombOff + 2 * kWaves * 64) * sizeof(float) <= kSlotBytes, "split combine buffers fit the slots");
 
 // three-value block reduction (min, max, max) for the record header (blockDim.x / 64 <= 16 waves)
 __device__ __forceinline__ void header_reduce(float& rmin, float& rmax, float& spread, float* dst) {
@@ -632,6 +640,10 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
   const float QMIN = k2 * 1e-6f;
   float acc[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   const f32x4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
+  if (nrb == 0) {  // an empty quarter of a split block
+    __builtin_amdgcn_wave_barrier();
+    return 0.0f;
+  }
   const float* wsrc = Wt + (FIXED ? 16 : 0) + 4 * g;
   auto load_a = [&](int rb) { return __builtin_bit_cast(bf16x8, At[rb * 64 + lane]); };
   auto load_w = [&](int rb) { return *reinterpret_cast<const float4*>(wsrc + rb * 32); };
@@ -681,14 +693,46 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
   return own;
 }
 
+// Split march (RM_MARCH_SPLIT): wave w of a block sums the row blocks [quarter_rb(w),
+// quarter_rb(w + 1)) (even bounds: lse_mfma runs pairs) and the four partial sums are added in
+// wave order, so every wave gets the same total. comb: 64 floats per wave of LDS.
+__device__ __forceinline__ int quarter_rb(int nrb, int w) { return ((nrb * w) / 4) & ~1; }
+__device__ __forceinline__ float split_combine(float part, float* comb, int wave, int lane) {
+  comb[wave * 64 + lane] = part;
+  __syncthreads();
+  return ((comb[lane] + comb[64 + lane]) + comb[128 + lane]) + comb[192 + lane];
+}
+// The matrix-core sum over all row blocks as a split block forms it: the four quarters' sums
+// added in wave order (one wave computing every quarter: the origin step of a split launch).
+template <bool CLAMP, bool FIXED>
+__device__ __forceinline__ float lse_mfma_quarters(const float p[3], float k2, float sh, const uint4* __restrict__ At,
+                                                   const float* __restrict__ Wt, int nrb, uint4* xa, uint4* xb,
+                                                   float* xs, int lane) {
+  float q[4];
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const int r0 = quarter_rb(nrb, w), r1 = quarter_rb(nrb, w + 1);
+    q[w] = lse_mfma<CLAMP, FIXED>(p, k2, sh, At + (size_t)r0 * 64, Wt + (size_t)r0 * 32, r1 - r0, xa, xb, xs, lane);
+  }
+  return ((q[0] + q[1]) + q[2]) + q[3];
+}
+
 // A march step's soft-min D at p on the matrix cores without a shift (soft_min_march's
-// unshifted step; shared with write_origins like march_d_fixed).
+// unshifted step; shared with write_origins like march_d_fixed). comb != nullptr: a split
+// block's wave, At / Wt / nrb its quarter (split_combine); quarters: all quarters in one wave.
 template <bool CLAMP>
 __device__ __forceinline__ float march_d_none(const float p[3], float kappa, float inv_kappa,
                                               const uint4* __restrict__ At, const float* __restrict__ Wt, int nrb,
-                                              uint4* xa, uint4* xb, float* xs, int lane) {
+                                              uint4* xa, uint4* xb, float* xs, int lane, float* comb = nullptr,
+                                              int wave = 0, bool quarters = false) {
 #pragma clang fp contract(off)
-  const float s = lse_mfma<CLAMP, false>(p, kappa * kappa, 0.0f, At, Wt, nrb, xa, xb, xs, lane);
+  float s;
+  if (quarters) {
+    s = lse_mfma_quarters<CLAMP, false>(p, kappa * kappa, 0.0f, At, Wt, nrb, xa, xb, xs, lane);
+  } else {
+    s = lse_mfma<CLAMP, false>(p, kappa * kappa, 0.0f, At, Wt, nrb, xa, xb, xs, lane);
+    if (comb != nullptr) s = split_combine(s, comb, wave, lane);
+  }
   return -flog2(fmaxf(s, 1e-30f)) * inv_kappa;
 }
 
@@ -707,11 +751,18 @@ template <bool CLAMP>
 __device__ __forceinline__ float march_d_fixed(const float p[3], float kappa, float inv_kappa, float kr_first,
                                                const float4& S00, const float4& S10, const uint4* __restrict__ At,
                                                const float* __restrict__ Wt, int nrb, uint4* xa, uint4* xb,
-                                               float* xs, int lane) {
+                                               float* xs, int lane, float* comb = nullptr, int wave = 0,
+                                               bool quarters = false) {
 #pragma clang fp contract(off)
   const float k2 = kappa * kappa;
   const float sh = fixed_shift(p, k2, S00, S10);
-  const float s = lse_mfma<CLAMP, true>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
+  float s;
+  if (quarters) {
+    s = lse_mfma_quarters<CLAMP, true>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
+  } else {
+    s = lse_mfma<CLAMP, true>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
+    if (comb != nullptr) s = split_combine(s, comb, wave, lane);
+  }
   const float m = kr_first - sh;
   return -(flog2(fmaxf(s, 1e-30f)) + m) * inv_kappa;
 }
@@ -741,10 +792,12 @@ __device__ void write_origins(const KArgs& a, const float4& S00, const float4& S
     // the first step's choice in soft_min_march: unshifted when sphere 0 proves it safe, else
     // the fixed shift (else the vector path: not shared)
     const bool none = a.mfma && shift_none_ok && fixed_shift(p, kappa * kappa, S00, S10) - kr_first <= 90.0f;
+    // (a split launch's first step adds the four quarters' sums: the same here)
     if (none)
-      D = march_d_none<true>(p, kappa, inv_kappa, At, Wt, np / 8, xa, xb, xs, lane);
+      D = march_d_none<true>(p, kappa, inv_kappa, At, Wt, np / 8, xa, xb, xs, lane, nullptr, 0, a.split != 0);
     else if (a.mfma && shift_fixed_ok && psq(p) <= 1e10f)
-      D = march_d_fixed<true>(p, kappa, inv_kappa, kr_first, S00, S10, At, Wt, np / 8, xa, xb, xs, lane);
+      D = march_d_fixed<true>(p, kappa, inv_kappa, kr_first, S00, S10, At, Wt, np / 8, xa, xb, xs, lane, nullptr, 0,
+                              a.split != 0);
     if (lane == 0) orig[v] = D;
   }
 }
@@ -1046,7 +1099,7 @@ __device__ __forceinline__ long long ray_block(const KArgs& a) {
 // dearest blocks; cost in march-step units, see the hand-off in rm_ray_kernel).
 __device__ __forceinline__ void order_append(const KArgs& a, long long blk, int cost) {
   constexpr int kCls = RM_ORDER_CLASSES;
-  const float cls_scale = (float)kCls / (float)(kWaves * (a.steps + kPostCost) + 1);
+  const float cls_scale = (float)kCls / (float)((a.split ? 1 : kWaves) * (a.steps + kPostCost) + 1);
   const int c = kCls - 1 - (int)fminf((float)cost * cls_scale, (float)(kCls - 1));
   const int idx = atomicAdd(a.ocnt_w + c, 1);
   // counts left uncleared (a failed launch in the rotation) overrun the total, and ray_block
@@ -1146,18 +1199,19 @@ __global__ __launch_bounds__(kBlock) void rm_escape_kernel(const KArgs a, int* _
   if (tid == 0) flags[blk] = all;
 }
 
-template <int MODE, bool CAM>
+template <int MODE, bool CAM, bool SPLIT>
 __device__ __forceinline__ void ray_body(const KArgs& a);
 
 // The per-ray kernel. Measurement build (-DRM_BLOCK_TRACE): every wave also records {start, end}
 // (s_memrealtime, 100 MHz), its hardware slot (HW_ID | XCC_ID << 32), {logical block, launch
 // position}, the times its march and its post-march forward ended and its march steps saved into
 // a.btrace[kTraceWords * (blockIdx.x * kWaves + wave) ...] (tools/block_trace.py).
-template <int MODE, bool CAM>
+// SPLIT: the split march (RM_MARCH_SPLIT, KArgs::split).
+template <int MODE, bool CAM, bool SPLIT>
 __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const KArgs a) {
 #ifdef RM_BLOCK_TRACE
   const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
-  ray_body<MODE, CAM>(a);
+  ray_body<MODE, CAM, SPLIT>(a);
   const unsigned long long t_end = __builtin_amdgcn_s_memrealtime();
   if (a.btrace != nullptr && (threadIdx.x & 63) == 0) {
     const unsigned hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_REG_HW_ID
@@ -1169,11 +1223,17 @@ __global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const 
     r[3] = (unsigned long long)ray_block(a) | ((unsigned long long)blockIdx.x << 32);
   }
 #else
-  ray_body<MODE, CAM>(a);
+  ray_body<MODE, CAM, SPLIT>(a);
 #endif
 }
 
-template <int MODE, bool CAM>
+// Split march (SPLIT): a block takes 64 rays (one 8x8 quadrant of a 16x16 tile in camera mode)
+// and all four of its waves hold them; every march step each wave sums a quarter of the sphere
+// row blocks on the matrix cores and the quarters are added in wave order (split_combine), so
+// the four waves march in lockstep through identical decisions (shift, clamp, exit). After the
+// march only wave 0 goes on (post-march forward, backward); the others end as escaped waves
+// with zero contributions. A ray that marches every step then occupies four SIMDs instead of one.
+template <int MODE, bool CAM, bool SPLIT>
 __device__ __forceinline__ void ray_body(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   Lds L;
@@ -1195,9 +1255,11 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long long blk = ray_block(a);
-  const long long li = blk * kBlock + tid;
+  const long long li = SPLIT ? blk * 64 + lane : blk * kBlock + tid;
   const bool valid = li < a.n_rays;
   long long ri = a.ray_begin + (valid ? li : 0);  // becomes the ray's row in the [N,3] tensors
+  // the wave that writes this ray's outputs and runs its post-march forward and backward
+  const bool own_rays = !SPLIT || wave == 0;
 
   const float kappa = a.k * kLog2e, nkappa = -kappa, inv_kappa = 1.0f / kappa;
 
@@ -1235,6 +1297,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   // choices: their outputs and gradient terms are exactly 0 whatever they compute.
   bool gone = false;
   auto all_safe = [&](float dist_lb) { return __all(dist_lb + rmin >= kSafeRho || gone) != 0; };
+  int split_par = 0;  // SPLIT: which of the two combine buffers the next step uses
 
   // every sweep visits all sphere pairs in one pass (records are not staged)
   auto for_tiles = [&](auto&& body) { body(0, a.Mpad); };
@@ -1275,13 +1338,24 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       tr_paths += 1ull << (16 * ((fixed ? 2 : 0) + (fast ? 0 : 1)));
 #endif
       float Dm;
+      const uint4* At = L.At;
+      const float* Wt = L.Wt;
+      int nq = nrb;
+      float* comb = nullptr;
+      if constexpr (SPLIT) {  // this wave's quarter of the row blocks; combine buffers alternate
+        const int r0 = quarter_rb(nrb, wave);
+        nq = quarter_rb(nrb, wave + 1) - r0;
+        At += (size_t)r0 * 64;
+        Wt += (size_t)r0 * 32;
+        comb = L.slots + kSplitCombOff + (split_par ^= 1) * (kWaves * 64);
+      }
       if (fixed) {  // the ray's shift: rho'_0 of sphere 0 (any value near it keeps +-100 headroom)
         const float4 A = Lds::v4(L.S0[0]), B = Lds::v4(L.S1[0]);
-        Dm = fast ? march_d_fixed<false>(p, kappa, inv_kappa, kr_first, A, B, L.At, L.Wt, nrb, xa, xb, xs, lane)
-                  : march_d_fixed<true>(p, kappa, inv_kappa, kr_first, A, B, L.At, L.Wt, nrb, xa, xb, xs, lane);
+        Dm = fast ? march_d_fixed<false>(p, kappa, inv_kappa, kr_first, A, B, At, Wt, nq, xa, xb, xs, lane, comb, wave)
+                  : march_d_fixed<true>(p, kappa, inv_kappa, kr_first, A, B, At, Wt, nq, xa, xb, xs, lane, comb, wave);
       } else {
-        Dm = fast ? march_d_none<false>(p, kappa, inv_kappa, L.At, L.Wt, nrb, xa, xb, xs, lane)
-                  : march_d_none<true>(p, kappa, inv_kappa, L.At, L.Wt, nrb, xa, xb, xs, lane);
+        Dm = fast ? march_d_none<false>(p, kappa, inv_kappa, At, Wt, nq, xa, xb, xs, lane, comb, wave)
+                  : march_d_none<true>(p, kappa, inv_kappa, At, Wt, nq, xa, xb, xs, lane, comb, wave);
       }
       (void)k2;
 #ifdef RM_BLOCK_TRACE
@@ -1436,11 +1510,12 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
 #if RM_PRIO_RAMP
   __builtin_amdgcn_s_setprio(1);
 #endif
-  if ((MODE == kFwd || MODE == kRender) && a.t_out != nullptr && valid) a.t_out[ri] = t;
+  if ((MODE == kFwd || MODE == kRender) && a.t_out != nullptr && valid && own_rays) a.t_out[ri] = t;
+  if (!own_rays) dead = true;  // SPLIT: waves 1-3 are done after the march (zero contributions)
   // work statistics: per wave here in the forward modes; per block at the hand-off barrier in the
   // backward modes (one pair of atomics per block, not per wave)
   if constexpr (MODE == kFwd || MODE == kRender) {
-    if (a.stats != nullptr && lane == 0) {
+    if (a.stats != nullptr && lane == 0 && own_rays) {
       if (dead) atomicAdd(a.stats + 1, 1ull);
       if (steps_saved != 0) atomicAdd(a.stats + 2, (unsigned long long)steps_saved);
     }
@@ -1559,14 +1634,14 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   const float scale = Lgt * mu;
   const float outv[3] = {mix[0] * scale, mix[1] * scale, mix[2] * scale};
 
-  if (MODE == kFwd && a.dbg != nullptr && valid) {
+  if (MODE == kFwd && a.dbg != nullptr && valid && own_rays) {
     float* q = a.dbg + 24 * ri;
     const float vals[24] = {t, tf, nrm[0], nrm[1], nrm[2], Lgt, mix[0], mix[1], mix[2], Df, mu, sdot, dmin,
                             Zw, Zb, 0.0f, D6[0], D6[1], D6[2], D6[3], D6[4], D6[5], 0.0f, 0.0f};
 #pragma unroll
     for (int c = 0; c < 24; ++c) q[c] = vals[c];
   }
-  const bool write_out = MODE != kBwd && a.out != nullptr && valid;
+  const bool write_out = MODE != kBwd && a.out != nullptr && valid && own_rays;
   if (write_out) {
     a.out[3 * ri] = outv[0];
     a.out[3 * ri + 1] = outv[1];
@@ -1581,7 +1656,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   // ---- seed g = dL/dout
   float g[3] = {0.0f, 0.0f, 0.0f};
   float loss = 0.0f;
-  if (valid) {
+  if (valid && own_rays) {
     if constexpr (MODE == kBwd) {
       g[0] = a.gout[3 * ri];
       g[1] = a.gout[3 * ri + 1];
@@ -1638,13 +1713,13 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     // the post-march forward and the backward (the next call's cost-ordered dispatch)
     int cost = 0;
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) cost += a.steps - wflag[kWaves + w] + (wflag[w] ? 0 : kPostCost);
+    for (int w = 0; w < (SPLIT ? 1 : kWaves); ++w) cost += a.steps - wflag[kWaves + w] + (wflag[w] ? 0 : kPostCost);
     order_append(a, blk, cost);
   }
   if (a.stats != nullptr && tid == 0) {
     int ex = 0, sv = 0;
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
+    for (int w = 0; w < (SPLIT ? 1 : kWaves); ++w) {
       ex += wflag[w];
       sv += wflag[kWaves + w];
     }
@@ -2353,8 +2428,9 @@ struct rm_context {
   void* rec = nullptr;                      // sphere records of the current call (rm_prep_kernel)
   size_t rec_bytes = 0;
   long long stats_blocks = 0;               // ray blocks launched while stats are on
+  long long stats_waves = 0;                // their ray waves (a split block holds one)
   int* block_order = nullptr;               // centre-out tile order for order_tx x order_ty tiles
-  int order_tx = 0, order_ty = 0;
+  int order_tx = 0, order_ty = 0, order_sub = 0;
   int* olist = nullptr;                     // cost-ordered dispatch: 3 x [class][kMaxBlocksPerLaunch] block lists
   int* ocnt = nullptr;                      // 3 x [class] list lengths (zeroed one launch ahead)
   int oturn = 0;                            // the list set the next keyed launch appends to
@@ -2391,10 +2467,9 @@ int fail(rm_context* ctx, int code, const char* fmt, ...) {
 // distance of the block's pixel-centre from the image centre, ties by block index. A block is a
 // whole tile (256-ray blocks) or one of its four 8x8 quadrants (64-ray blocks, RM_BLOCK=64), in
 // the pixel order of setup_ray. Built once per image size.
-int ensure_block_order(rm_context* ctx, int tx, int ty) {
-  if (ctx->block_order && ctx->order_tx == tx && ctx->order_ty == ty) return RM_OK;
-  constexpr int sub = 256 / kBlock;  // blocks per 16x16 tile
-  static_assert(sub == 1 || sub == 4, "ray blocks are 16x16 tiles or their 8x8 quadrants");
+int ensure_block_order(rm_context* ctx, int tx, int ty, int sub) {
+  if (ctx->block_order && ctx->order_tx == tx && ctx->order_ty == ty && ctx->order_sub == sub) return RM_OK;
+  // sub = ray blocks per 16x16 tile: 1 (256-ray blocks) or 4 (8x8 quadrants: 64-ray blocks, split)
   std::vector<int> ord((size_t)tx * ty * sub);
   for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
   auto key = [&](int i) {  // twice the pixel offset of the block centre from the image centre
@@ -2426,6 +2501,7 @@ int ensure_block_order(rm_context* ctx, int tx, int ty) {
   RM_HIP(ctx, hipMemcpy(ctx->block_order, ord.data(), sizeof(int) * ord.size(), hipMemcpyHostToDevice));
   ctx->order_tx = tx;
   ctx->order_ty = ty;
+  ctx->order_sub = sub;
   return RM_OK;
 }
 
@@ -2441,9 +2517,9 @@ long long max_blocks_per_launch() {
 
 long long rec_floats(int Mpad) { return (long long)Mpad * 12 + 8; }
 
-size_t ws_need(long long max_rays, int M) {
+size_t ws_need(long long max_rays, int M, int rays_per_block = kBlock) {
   const int Mpad = pad_spheres(M);
-  long long blocks = (max_rays + kBlock - 1) / kBlock;
+  long long blocks = (max_rays + rays_per_block - 1) / rays_per_block;
   blocks = std::min<long long>(blocks, kMaxBlocksPerLaunch);
   const long long rec = rec_floats(Mpad);
   return (size_t)(blocks * rec + (long long)kReduceSegs * rec + 4096) * sizeof(float);
@@ -2550,13 +2626,19 @@ void launch_escape(bool cam, dim3 grid, hipStream_t st, const KArgs& a, int* fla
 }
 
 template <int MODE>
-void launch_ray(bool cam, dim3 grid, size_t lds, hipStream_t st, const KArgs& a, hipEvent_t ev0, hipEvent_t ev1) {
+void launch_ray(bool cam, bool split, dim3 grid, size_t lds, hipStream_t st, const KArgs& a, hipEvent_t ev0,
+                hipEvent_t ev1) {
   // With timing on, the start/stop timestamps come from the kernel's own dispatch packet
   // (hipExtLaunchKernel): no extra barrier packets or cache flushes around the launch.
-  if (cam)
-    hipExtLaunchKernelGGL((rm_ray_kernel<MODE, true>), grid, dim3(kBlock), (uint32_t)lds, st, ev0, ev1, 0u, a);
-  else
-    hipExtLaunchKernelGGL((rm_ray_kernel<MODE, false>), grid, dim3(kBlock), (uint32_t)lds, st, ev0, ev1, 0u, a);
+  const dim3 blk(kBlock);
+  const uint32_t sh = (uint32_t)lds;
+  if (split) {
+    if (cam) hipExtLaunchKernelGGL((rm_ray_kernel<MODE, true, true>), grid, blk, sh, st, ev0, ev1, 0u, a);
+    else hipExtLaunchKernelGGL((rm_ray_kernel<MODE, false, true>), grid, blk, sh, st, ev0, ev1, 0u, a);
+  } else {
+    if (cam) hipExtLaunchKernelGGL((rm_ray_kernel<MODE, true, false>), grid, blk, sh, st, ev0, ev1, 0u, a);
+    else hipExtLaunchKernelGGL((rm_ray_kernel<MODE, false, false>), grid, blk, sh, st, ev0, ev1, 0u, a);
+  }
 }
 
 int run(rm_context* ctx, const Call& c) {
@@ -2623,7 +2705,20 @@ int run(rm_context* ctx, const Call& c) {
   // Escape skipping needs the mask to be exactly 0 at the certified distance: sigmoid(-msharp D)
   // once msharp log2(e) D > 128 overflows exp2 (use 160), exp(-10 D^2) in kRender long before 50.
   const bool mask_vanishes = c.mode == kRender || a.msharp > 0.0f;
-  a.cull = ((c.march->flags & RM_MARCH_SKIP_ESCAPED) != 0 && mask_vanishes && !c.t_out && !c.dbg) ? 1 : 0;
+  // Split march (RM_MARCH_SPLIT): forced by the flag or env RM_SPLIT=1, automatic from
+  // kSplitMinSpheres spheres when the launch fills the GPU at most about once; never with
+  // RM_MARCH_NO_SPLIT / env RM_SPLIT=0, in the renderer.rs mode or with the escape pre-pass.
+  bool split = false;
+  if (c.mode != kRender && (c.march->flags & RM_MARCH_SKIP_ESCAPED) == 0) {
+    const char* e = std::getenv("RM_SPLIT");
+    const long long n_all = c.cam ? (long long)c.views * c.W * c.H : c.n;
+    if ((c.march->flags & RM_MARCH_SPLIT) != 0 || (e && e[0] == '1')) split = true;
+    else if ((c.march->flags & RM_MARCH_NO_SPLIT) == 0 && !(e && e[0] == '0'))
+      split = M >= kSplitMinSpheres && n_all <= kSplitMaxRays;
+  }
+  a.split = split ? 1 : 0;
+  const int rpb = split ? 64 : kBlock;  // rays per block
+  a.cull = ((c.march->flags & RM_MARCH_SKIP_ESCAPED) != 0 && mask_vanishes && !c.t_out && !c.dbg && !split) ? 1 : 0;
   a.cull_min_d = c.mode == kRender ? 50.0f : std::max(50.0f, 160.0f / (a.msharp * 1.44269504f));
   a.lse_slack = (float)(std::log((double)M) / (double)a.k * (1.0 + 1e-6)) + 1e-7f;
   // Escaped-ray early exit: the mask must be exactly 0 at distance gone_d -- exp2 of
@@ -2681,7 +2776,7 @@ int run(rm_context* ctx, const Call& c) {
   const size_t lds = lds_bytes();
 
   if (has_bwd) {
-    if ((rc = ensure_ws(ctx, ws_need(std::max<long long>(n, 1), M))) != RM_OK) return rc;
+    if ((rc = ensure_ws(ctx, ws_need(std::max<long long>(n, 1), M, rpb))) != RM_OK) return rc;
   }
   float* P = static_cast<float*>(ctx->ws);
 
@@ -2691,14 +2786,17 @@ int run(rm_context* ctx, const Call& c) {
   long long done = 0;
   bool first = true;
   do {
-    const long long blocks_left = (n - done + kBlock - 1) / kBlock;
+    const long long blocks_left = (n - done + rpb - 1) / rpb;
     const long long nb = std::min<long long>(blocks_left, max_blocks_per_launch());
-    const long long nr = std::min<long long>(n - done, nb * kBlock);
+    const long long nr = std::min<long long>(n - done, nb * rpb);
     a.ray_begin = done;
     a.n_rays = nr;
     a.partials = P;
     a.stats = ctx->stats_dev;
-    if (ctx->stats_dev) ctx->stats_blocks += nb;
+    if (ctx->stats_dev) {
+      ctx->stats_blocks += nb;
+      ctx->stats_waves += nb * (split ? 1 : kWaves);
+    }
     a.esc_flags = nullptr;
     a.block_order = nullptr;
     a.olist_r = nullptr;
@@ -2707,12 +2805,12 @@ int run(rm_context* ctx, const Call& c) {
     a.ocnt_w = nullptr;
     a.ocnt_z = nullptr;
     const long long npix = (long long)c.W * c.H;
-    if (c.cam && a.tiling == 2 && nb > 1 && done % npix == 0 && nr % npix == 0 && nr == nb * kBlock &&
+    if (c.cam && a.tiling == 2 && nb > 1 && done % npix == 0 && nr % npix == 0 && nr == nb * rpb &&
         (c.march->flags & RM_MARCH_NATURAL_ORDER) == 0) {
-      if ((rc = ensure_block_order(ctx, c.W / 16, c.H / 16)) != RM_OK) return rc;
+      if ((rc = ensure_block_order(ctx, c.W / 16, c.H / 16, 256 / rpb)) != RM_OK) return rc;
       a.block_order = ctx->block_order;
       a.order_views = (int)(nr / npix);
-      a.order_tiles = (int)(npix / kBlock);
+      a.order_tiles = (int)(npix / rpb);
     }
     // cost-ordered dispatch from the previous launch over the same views (single-launch calls)
     const bool has_rec = c.mode == kBwd || c.mode == kTrain;
@@ -2720,7 +2818,7 @@ int run(rm_context* ctx, const Call& c) {
     if (a.block_order != nullptr && has_rec && nb == blocks_left && done == 0 &&
         (c.march->flags & RM_MARCH_STATIC_ORDER) == 0) {
       key = ((unsigned long long)c.W << 48) ^ ((unsigned long long)c.H << 32) ^ ((unsigned long long)c.views << 24) ^
-            ((unsigned long long)Mpad << 1) ^ 1ull;
+            ((unsigned long long)Mpad << 1) ^ 1ull ^ ((unsigned long long)split << 2);
       constexpr int kCls = RM_ORDER_CLASSES;
       if (!ctx->olist) {
         RM_HIP(ctx, hipMalloc(&ctx->olist, sizeof(int) * 3 * kCls * kMaxBlocksPerLaunch));
@@ -2776,10 +2874,10 @@ int run(rm_context* ctx, const Call& c) {
       a.btrace = ctx->btrace;
       ctx->btrace_waves = nb * kWaves;
 #endif
-      if (c.mode == kFwd) launch_ray<kFwd>(c.cam, grid, lds, ctx->stream, a, ev0, ev1);
-      else if (c.mode == kBwd) launch_ray<kBwd>(c.cam, grid, lds, ctx->stream, a, ev0, ev1);
-      else if (c.mode == kTrain) launch_ray<kTrain>(c.cam, grid, lds, ctx->stream, a, ev0, ev1);
-      else launch_ray<kRender>(c.cam, grid, lds, ctx->stream, a, ev0, ev1);
+      if (c.mode == kFwd) launch_ray<kFwd>(c.cam, split, grid, lds, ctx->stream, a, ev0, ev1);
+      else if (c.mode == kBwd) launch_ray<kBwd>(c.cam, split, grid, lds, ctx->stream, a, ev0, ev1);
+      else if (c.mode == kTrain) launch_ray<kTrain>(c.cam, split, grid, lds, ctx->stream, a, ev0, ev1);
+      else launch_ray<kRender>(c.cam, false, grid, lds, ctx->stream, a, ev0, ev1);
       RM_HIP(ctx, hipGetLastError());
     }
     if (has_bwd) {
@@ -2899,6 +2997,7 @@ int rm_stats_enable(rm_context* ctx, int32_t enable) {
     RM_HIP(ctx, hipMalloc(&ctx->stats_dev, 4 * sizeof(unsigned long long)));
     RM_HIP(ctx, hipMemsetAsync(ctx->stats_dev, 0, 4 * sizeof(unsigned long long), ctx->stream));
     ctx->stats_blocks = 0;
+    ctx->stats_waves = 0;
   } else if (!enable && ctx->stats_dev) {
     RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
     RM_HIP(ctx, hipFree(ctx->stats_dev));
@@ -2915,7 +3014,7 @@ int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset) {
   RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
   out->blocks = ctx->stats_blocks;
   out->blocks_skipped = (int64_t)v[0];
-  out->waves = ctx->stats_blocks * kWaves;
+  out->waves = ctx->stats_waves;
   out->waves_exited = (int64_t)v[1];
   out->steps_saved = (int64_t)v[2];
 #ifdef RM_LANE_STATS
@@ -2924,6 +3023,7 @@ int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset) {
   if (reset) {
     RM_HIP(ctx, hipMemsetAsync(ctx->stats_dev, 0, sizeof v, ctx->stream));
     ctx->stats_blocks = 0;
+    ctx->stats_waves = 0;
   }
   return RM_OK;
 }

@@ -42,6 +42,8 @@ RM_MARCH_PER_RAY_ORIGIN = 32
 RM_MARCH_STATIC_ORDER = 64
 RM_MARCH_FORCE_MAX_SHIFT = 128
 RM_MARCH_COLOR_F16 = 256
+RM_MARCH_SPLIT = 512
+RM_MARCH_NO_SPLIT = 1024
 
 
 class RmStats(ctypes.Structure):

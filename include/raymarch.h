@@ -116,6 +116,17 @@ typedef struct rm_march {
  * the colour blend, the SDF, the march and every gradient stay fp32 (grads->colors is fp32,
  * the master gradient). See rm_optimizer_step_f16 for the optimizer side. */
 #define RM_MARCH_COLOR_F16 256
+/* Split march: a ray block takes 64 rays (one 8x8 pixel quadrant in camera mode) held by all
+ * four waves of the block; every march step each wave sums a quarter of the spheres on the
+ * matrix cores and the quarters are added in a fixed order, so the waves march in lockstep;
+ * the post-march forward and the backward run on the first wave. A ray that marches every
+ * step then spreads over four SIMDs: for many spheres when one launch fills the GPU about once
+ * (BASELINE configs[4]), where a few rays march all steps while the rest leave early. Taken
+ * automatically from 2048 spheres for launches of at most 262,144 rays; this flag forces it,
+ * RM_MARCH_NO_SPLIT forbids it. Results agree to fp32 rounding (the sphere sums are added in
+ * another order). */
+#define RM_MARCH_SPLIT 512
+#define RM_MARCH_NO_SPLIT 1024
 
 /* Pinhole LookAt camera, camera.rs:30-37. Rays are generated in-kernel exactly as
  * create_camera_rays (camera.rs:41-87): rows y then x, u = x/W*2-1, v = -(y/H*2-1). */

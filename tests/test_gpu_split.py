@@ -1,0 +1,166 @@
+"""Split march (RM_MARCH_SPLIT / env RM_SPLIT=1): 64 rays per block held by all four waves, each
+wave summing a quarter of the sphere row blocks per march step, the quarters added in wave order.
+
+  * against the fp64 oracle (forward, backward, train step) at sphere counts whose row blocks
+    split evenly (256), unevenly (300: quarters of 4, 6, 4, 6 row blocks) and over many tiles
+    (1100), and the split path really runs (its images differ from the unsplit ones in the last
+    bits);
+  * bit-for-bit properties the unsplit march has too: early exit on / off, shared origin step /
+    per-ray first step, three consecutive train calls (the 2nd and 3rd in the cost order of the
+    call before), camera mode in row order / array mode on the same rays, ragged ray counts;
+  * the automatic choice (>= 2048 spheres, <= 262,144 rays per launch) and RM_MARCH_NO_SPLIT.
+Tolerances as in tests/test_gpu_parity.py.
+"""
+import numpy as np
+import pytest
+
+from conftest import gpu_available
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
+
+FWD_MAX, FWD_MEAN = 1e-3, 1e-5
+GRAD_TOL = {"centers": 3e-3, "radius": 3e-3, "colors": 3e-3, "light_dir": 1e-2, "ambient": 3e-3}
+KEYS = ("centers", "colors", "radius", "light_dir", "ambient")
+
+
+@pytest.fixture(scope="module")
+def rm():
+    import torch
+    from burn_raymarching_amd import _build
+    _build.build_lib()
+    from burn_raymarching_amd import model, native, render
+    torch.cuda.init()
+    return render, model, native
+
+
+def dev(x):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(x, np.float32)).cuda()
+
+
+def host(t):
+    return t.detach().float().cpu().numpy()
+
+
+def check_fwd(got, ref):
+    e = np.abs(got.astype(np.float64) - ref)
+    assert np.isfinite(got).all()
+    assert e.max() <= FWD_MAX and e.mean() <= FWD_MEAN, (e.max(), e.mean())
+
+
+def check_grads(got, ref):
+    for key, tol in GRAD_TOL.items():
+        a = host(got[key]).reshape(-1).astype(np.float64)
+        b = np.asarray(ref[key]).reshape(-1)
+        bound = tol * max(np.abs(b).max(), 1e-12)
+        assert np.abs(a - b).max() <= bound, (key, np.abs(a - b).max(), bound)
+
+
+def cam_rays(oracle, cams, w, h):
+    rays = [oracle.camera_rays(w, h, *c, precision="f32") for c in cams]
+    return np.concatenate([r[0] for r in rays]), np.concatenate([r[1] for r in rays])
+
+
+@pytest.mark.parametrize("m", [256, 300, 1100])
+def test_split_against_oracle(rm, oracle, monkeypatch, m):
+    import torch
+    render, model, _ = rm
+    W = H = 48
+    S, K = 32, 32.0
+    sc = model.synthetic_scene(m, 11, radius_range=(0.02, 0.08))
+    cams = model.ring_cameras(10, offset=4)[:2]
+    o, d = cam_rays(oracle, cams, W, H)
+    o64, d64 = o.astype(np.float64), d.astype(np.float64)
+    s = model.scene_tensors(sc)
+    monkeypatch.setenv("RM_SPLIT", "0")
+    unsplit = render.render_diff_camera(cams, W, H, s, K, S)
+    monkeypatch.setenv("RM_SPLIT", "1")
+    out = render.render_diff_camera(cams, W, H, s, K, S)
+    assert not torch.equal(out, unsplit)  # the quarters' sums are added in another order
+    check_fwd(host(out), oracle.render_diff(o64, d64, sc, S, K))
+    g = np.random.default_rng(3).normal(size=o.shape).astype(np.float32)
+    check_grads(render.render_diff_backward_camera(cams, W, H, s, K, dev(g), S),
+                oracle.render_diff_backward(o64, d64, sc, S, K, g.astype(np.float64)))
+    targets = oracle.render_diff(o64, d64, model.synthetic_scene(m, 12, radius_range=(0.02, 0.08)), S,
+                                 K).astype(np.float32)
+    for _ in range(2):  # the 2nd call in the cost order of the 1st
+        loss, gt, _ = render.train_step_camera(cams, W, H, dev(targets), s, K, 0.4, S)
+    _, loss_ref, g_ref = oracle.train_step(o64, d64, targets.astype(np.float64), sc, S, K, 0.4)
+    assert abs(host(loss)[0] - loss_ref) <= 1e-4 * abs(loss_ref)
+    check_grads(gt, g_ref)
+
+
+def _train(render, native, cams, w, h, tg, s, k, steps, flags=0):
+    import torch
+    out = torch.empty_like(tg)
+    loss, g, _ = render.train_step_camera(cams, w, h, tg, s, k, 0.3, steps, out=out,
+                                          march=native.march_params(steps, k, flags=flags))
+    torch.cuda.synchronize()
+    return host(loss), {key: host(v) for key, v in g.items()}, host(out)
+
+
+def _equal(a, b):
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[2], b[2])
+    for key in KEYS:
+        assert np.array_equal(a[1][key], b[1][key]), key
+
+
+def test_split_bitwise_properties(rm, monkeypatch):
+    render, model, native = rm
+    W = H = 64
+    M, S, K = 300, 40, 32.0
+    sc = model.scene_tensors(model.synthetic_scene(M, 13))
+    cams = model.ring_cameras(10, offset=6)[:2]
+    tg = render.render_diff_camera(cams, W, H, model.scene_tensors(model.synthetic_scene(M, 14)), K, S)
+    monkeypatch.setenv("RM_SPLIT", "1")
+    base = _train(render, native, cams, W, H, tg, sc, K, S)
+    # three consecutive calls: the later ones in the cost order of the one before
+    _equal(base, _train(render, native, cams, W, H, tg, sc, K, S))
+    _equal(base, _train(render, native, cams, W, H, tg, sc, K, S))
+    # early exit off
+    _equal(base, _train(render, native, cams, W, H, tg, sc, K, S, flags=native.RM_MARCH_NO_EARLY_EXIT))
+    # per-ray first step instead of the shared origin step
+    _equal(base, _train(render, native, cams, W, H, tg, sc, K, S, flags=native.RM_MARCH_PER_RAY_ORIGIN))
+    # static dispatch order
+    _equal(base, _train(render, native, cams, W, H, tg, sc, K, S, flags=native.RM_MARCH_STATIC_ORDER))
+
+
+def test_split_array_mode_and_ragged(rm, oracle, monkeypatch):
+    """Array mode on the rays of a row-order camera launch gives the same image bit for bit, and
+    ragged ray counts (a last block with 1..63 rays) stay within the oracle's tolerance."""
+    import torch
+    render, model, native = rm
+    W, H = 40, 24
+    M, S, K = 256, 24, 32.0
+    sc = model.synthetic_scene(M, 15)
+    s = model.scene_tensors(sc)
+    cams = model.ring_cameras(10, offset=2)[:1]
+    monkeypatch.setenv("RM_SPLIT", "1")
+    monkeypatch.setenv("RM_ROW_ORDER", "1")
+    cam_out = render.render_diff_camera(cams, W, H, s, K, S)
+    o, d = cam_rays(oracle, cams, W, H)
+    arr_out = render.render_diff_forward(dev(o), dev(d), s, K, S)
+    assert torch.equal(cam_out, arr_out)
+    for n in (1, 63, 65, 777):
+        out = render.render_diff_forward(dev(o[:n]), dev(d[:n]), s, K, S)
+        check_fwd(host(out), oracle.render_diff(o[:n].astype(np.float64), d[:n].astype(np.float64), sc, S, K))
+
+
+def test_split_automatic_choice(rm, monkeypatch):
+    """From 2048 spheres the split march is taken automatically for launches of at most 262,144
+    rays (the same bits as RM_SPLIT=1); RM_MARCH_NO_SPLIT gives the unsplit bits."""
+    render, model, native = rm
+    M, S, K = 2048, 16, 32.0
+    s = model.scene_tensors(model.synthetic_scene(M, 16, radius_range=(0.01, 0.04)))
+    cams = model.ring_cameras(10)[:1]
+    tg = render.render_diff_camera(cams, 32, 32, model.scene_tensors(model.synthetic_scene(M, 17)), K, S)
+    monkeypatch.delenv("RM_SPLIT", raising=False)
+    auto = _train(render, native, cams, 32, 32, tg, s, K, S)
+    no = _train(render, native, cams, 32, 32, tg, s, K, S, flags=native.RM_MARCH_NO_SPLIT)
+    monkeypatch.setenv("RM_SPLIT", "1")
+    forced = _train(render, native, cams, 32, 32, tg, s, K, S)
+    monkeypatch.setenv("RM_SPLIT", "0")
+    off = _train(render, native, cams, 32, 32, tg, s, K, S)
+    _equal(auto, forced)
+    _equal(no, off)
+    assert not np.array_equal(auto[2], off[2])
