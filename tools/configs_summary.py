@@ -35,7 +35,7 @@ def main():
             for row in rows:
                 kern[row["Name"][:90]] = {"calls": int(row["Calls"]), "avg_us": round(float(row["AverageNs"]) / 1e3, 2)}
             entry["rocprof_kernels"] = kern
-            train = next((v for k, v in kern.items() if "rm_ray_kernel<2, true>" in k), None)
+            train = next((v for k, v in kern.items() if "rm_ray_kernel<2, true" in k), None)
             if train:
                 entry["rocprof_train_avg_us"] = train["avg_us"]
                 steps = train["calls"]

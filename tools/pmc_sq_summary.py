@@ -26,7 +26,7 @@ import json
 import os
 import sys
 
-KERNEL = "rm_ray_kernel<2, true>"
+KERNEL = "rm_ray_kernel<2, true"  # <2, true, SPLIT>: the camera-mode train kernel
 TRANS_CYCLES = 8.6    # cycles per transcendental wave-instruction per SIMD (r01_valu_rates.txt)
 OTHER_CYCLES = 4.0    # other VALU: fma 2.96, add 3.56, max 4.45, packed fma 5.02 (r01_valu_rates.txt)
 SIMDS = 1024          # 256 CUs x 4 SIMDs

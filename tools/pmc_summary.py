@@ -35,7 +35,7 @@ def main():
     fetch_dir, write_dir, out, key = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4]
     f = per_kernel(fetch_dir, "FETCH_SIZE")
     w = per_kernel(write_dir, "WRITE_SIZE")
-    name = next((k for k in f if "rm_ray_kernel<2, true>" in k), None)
+    name = next((k for k in f if "rm_ray_kernel<2, true" in k), None)
     if name is None:
         raise SystemExit("train kernel not found in the counter CSVs")
     fk = sum(f[name]) / len(f[name])
