@@ -74,6 +74,11 @@ constexpr int kMaxBlocksPerLaunch = 16384 * (256 / kBlock);
 // automatic split march (RM_MARCH_SPLIT): from this many spheres, for launches of at most this
 // many rays (about one fill of the GPU: 1024 resident 256-ray blocks)
 constexpr int kSplitMinSpheres = 2048;
+#ifndef RM_SPLIT_WAVES
+#define RM_SPLIT_WAVES 4
+#endif
+constexpr int kSplitWaves = RM_SPLIT_WAVES;  // waves per 64-ray block of the split march (2 or 4)
+static_assert(kSplitWaves == 2 || kSplitWaves == 4, "split blocks have 2 or 4 waves");
 constexpr long long kSplitMaxRays = 262144;
 #ifndef RM_REDUCE_SEGS
 #define RM_REDUCE_SEGS 128
@@ -693,14 +698,18 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
   return own;
 }
 
-// Split march (RM_MARCH_SPLIT): wave w of a block sums the row blocks [quarter_rb(w),
-// quarter_rb(w + 1)) (even bounds: lse_mfma runs pairs) and the four partial sums are added in
-// wave order, so every wave gets the same total. comb: 64 floats per wave of LDS.
-__device__ __forceinline__ int quarter_rb(int nrb, int w) { return ((nrb * w) / 4) & ~1; }
+// Split march (RM_MARCH_SPLIT): the kSplitWaves waves of a block hold the same 64 rays; wave w
+// sums the row blocks [part_rb(w), part_rb(w + 1)) (even bounds: lse_mfma runs pairs) and the
+// partial sums are added in wave order, so every wave gets the same total. comb: 64 floats per
+// wave of LDS.
+__device__ __forceinline__ int part_rb(int nrb, int w) { return ((nrb * w) / kSplitWaves) & ~1; }
 __device__ __forceinline__ float split_combine(float part, float* comb, int wave, int lane) {
   comb[wave * 64 + lane] = part;
   __syncthreads();
-  return ((comb[lane] + comb[64 + lane]) + comb[128 + lane]) + comb[192 + lane];
+  float s = comb[lane];
+#pragma unroll
+  for (int w = 1; w < kSplitWaves; ++w) s += comb[w * 64 + lane];
+  return s;
 }
 // The matrix-core sum over all row blocks as a split block forms it: the four quarters' sums
 // added in wave order (one wave computing every quarter: the origin step of a split launch).
@@ -708,13 +717,15 @@ template <bool CLAMP, bool FIXED>
 __device__ __forceinline__ float lse_mfma_quarters(const float p[3], float k2, float sh, const uint4* __restrict__ At,
                                                    const float* __restrict__ Wt, int nrb, uint4* xa, uint4* xb,
                                                    float* xs, int lane) {
-  float q[4];
+  float s = 0.0f;
 #pragma unroll
-  for (int w = 0; w < 4; ++w) {
-    const int r0 = quarter_rb(nrb, w), r1 = quarter_rb(nrb, w + 1);
-    q[w] = lse_mfma<CLAMP, FIXED>(p, k2, sh, At + (size_t)r0 * 64, Wt + (size_t)r0 * 32, r1 - r0, xa, xb, xs, lane);
+  for (int w = 0; w < kSplitWaves; ++w) {
+    const int r0 = part_rb(nrb, w), r1 = part_rb(nrb, w + 1);
+    const float q = lse_mfma<CLAMP, FIXED>(p, k2, sh, At + (size_t)r0 * 64, Wt + (size_t)r0 * 32, r1 - r0, xa, xb, xs,
+                                           lane);
+    s = w == 0 ? q : s + q;
   }
-  return ((q[0] + q[1]) + q[2]) + q[3];
+  return s;
 }
 
 // A march step's soft-min D at p on the matrix cores without a shift (soft_min_march's
@@ -1343,8 +1354,8 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       int nq = nrb;
       float* comb = nullptr;
       if constexpr (SPLIT) {  // this wave's quarter of the row blocks; combine buffers alternate
-        const int r0 = quarter_rb(nrb, wave);
-        nq = quarter_rb(nrb, wave + 1) - r0;
+        const int r0 = part_rb(nrb, wave);
+        nq = part_rb(nrb, wave + 1) - r0;
         At += (size_t)r0 * 64;
         Wt += (size_t)r0 * 32;
         comb = L.slots + kSplitCombOff + (split_par ^= 1) * (kWaves * 64);
@@ -1458,6 +1469,9 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     int st0 = 0;
 #ifdef RM_BLOCK_TRACE
     const unsigned long long tr_c_begin = __builtin_readcyclecounter();
+    float tr_cyc_t1 = __builtin_nanf(""), tr_cyc_t2 = __builtin_nanf(""), tr_cyc_d1 = __builtin_nanf(""),
+          tr_cyc_d2 = __builtin_nanf("");
+    int tr_cyc_first = -1;
 #endif
     if constexpr (CAM) {
       // Camera mode: step 0 from the soft-min at the eye, evaluated once per view by the same
@@ -1479,6 +1493,9 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
         }
       }
     }
+    // march states (t, Dprev) one and two steps back (the cycle exit)
+    float cyc_t1 = __builtin_nanf(""), cyc_t2 = __builtin_nanf(""), cyc_d1 = __builtin_nanf(""),
+          cyc_d2 = __builtin_nanf("");
     for (int st = st0; !dead && st < a.steps; ++st) {
 #if RM_PRIO_RAMP
       if (st == half) __builtin_amdgcn_s_setprio(2);
@@ -1488,6 +1505,40 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
         dead = true;
         break;
       }
+      // Cycle exit (exact): when every ray that is not gone repeats its march state (t, and the
+      // previous step's D, which the wave's choices depend on) of two steps earlier, the rest of
+      // the march repeats with period 2 (each step is a deterministic function of the wave's
+      // state; a ray cycling at a fixed distance cannot become gone later, the thresholds only
+      // grow), so the state after the last step is this one or the previous one by the parity of
+      // the steps left. Gone rays take their remaining bound steps here, as the march would.
+      if (a.early_exit && __all(gone || (t == cyc_t2 && Dprev == cyc_d2))) {
+        const int left = a.steps - st;
+        if (!gone && (left & 1)) {
+          t = cyc_t1;
+          Dprev = cyc_d1;
+          lb = Dprev - fabsf(Dprev);
+        }
+        if (gone)
+          for (int k = st; k < a.steps; ++k) {
+            const float q[3] = {fmaf(d[0], t, o[0]) - c0x, fmaf(d[1], t, o[1]) - c0y, fmaf(d[2], t, o[2]) - c0z};
+            t = fminf(t + (fsqrt(fmaf(q[2], q[2], fmaf(q[1], q[1], q[0] * q[0]))) - rprime), kTMax);
+          }
+        steps_saved += left;
+        break;
+      }
+      cyc_t2 = cyc_t1;
+      cyc_t1 = t;
+      cyc_d2 = cyc_d1;
+      cyc_d1 = Dprev;
+#ifdef RM_BLOCK_TRACE
+      // measurement: first step whose march state (t, D of the step before) repeats the state two
+      // steps earlier on every ray that is not gone (the march has entered a cycle of period <= 2)
+      if (tr_cyc_first < 0 && __all(gone || (t == tr_cyc_t2 && Dprev == tr_cyc_d2))) tr_cyc_first = st;
+      tr_cyc_t2 = tr_cyc_t1;
+      tr_cyc_t1 = t;
+      tr_cyc_d2 = tr_cyc_d1;
+      tr_cyc_d1 = Dprev;
+#endif
       const float D = soft_min_march(p, all_safe(lb), Dprev);
       t = fminf(t + (gone ? gone_step : D), kTMax);
       // next point: hard min >= soft-min D here, moved by |D|
@@ -1501,6 +1552,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   RM_TRACE(8, tr_lse_cyc);
   RM_TRACE(9, tr_vec);
   RM_TRACE(10, __builtin_readcyclecounter() - tr_c_begin);
+  RM_TRACE(11, (unsigned long long)(long long)tr_cyc_first);
 #endif
 #ifdef RM_LANE_STATS  // stats[3] += escaped lane-steps of the march + 5 sweeps per escaped lane of a live wave
     if (a.stats != nullptr && lane == 0)
@@ -1728,13 +1780,13 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   }
   int alive = 0;
 #pragma unroll
-  for (int w = 0; w < kWaves; ++w) alive |= wflag[w] ? 0 : (1 << w);
+  for (int w = 0; w < (SPLIT ? kSplitWaves : kWaves); ++w) alive |= wflag[w] ? 0 : (1 << w);
   if (dead) {
     if (alive == 0 && wave == 0) {  // the whole block escaped: scalar totals, live flag 0 (the
       if (lane < 8) {               // reduction skips the per-sphere columns, all zero)
         float acc = wscal[lane];
 #pragma unroll
-        for (int w = 1; w < kWaves; ++w) acc += wscal[w * 8 + lane];
+        for (int w = 1; w < (SPLIT ? kSplitWaves : kWaves); ++w) acc += wscal[w * 8 + lane];
         rec[(long long)a.Mpad * 12 + lane] = acc;
       }
     }
@@ -1747,7 +1799,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     float acc = 0.0f;
     bool first = true;
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w)
+    for (int w = 0; w < (SPLIT ? kSplitWaves : kWaves); ++w)
       if (alive & (1 << w)) {
         acc = first ? s0[w * stride] : acc + s0[w * stride];
         first = false;
@@ -2081,7 +2133,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   if (arank == 0 && lane < 8) {
     float acc = wscal[lane];
 #pragma unroll
-    for (int w = 1; w < kWaves; ++w) acc += wscal[w * 8 + lane];
+    for (int w = 1; w < (SPLIT ? kSplitWaves : kWaves); ++w) acc += wscal[w * 8 + lane];
     rec[(long long)a.Mpad * 12 + lane] = lane == 7 ? 1.0f : acc;  // scalar 7: live flag
   }
 }
@@ -2630,7 +2682,7 @@ void launch_ray(bool cam, bool split, dim3 grid, size_t lds, hipStream_t st, con
                 hipEvent_t ev1) {
   // With timing on, the start/stop timestamps come from the kernel's own dispatch packet
   // (hipExtLaunchKernel): no extra barrier packets or cache flushes around the launch.
-  const dim3 blk(kBlock);
+  const dim3 blk(split ? 64 * kSplitWaves : kBlock);
   const uint32_t sh = (uint32_t)lds;
   if (split) {
     if (cam) hipExtLaunchKernelGGL((rm_ray_kernel<MODE, true, true>), grid, blk, sh, st, ev0, ev1, 0u, a);

@@ -54,7 +54,8 @@ def run(args):
     buf = np.zeros((cap, 12), np.uint64)
     n = ctypes.c_int64()
     ctx.check(fn(ctx.handle, buf.ctypes.data, cap, ctypes.byref(n)), "rm_debug_block_trace")
-    return buf[:n.value]
+    tr = buf[:n.value]
+    return tr[tr[:, 0] != 0]  # split blocks of two waves leave the records of waves 2-3 empty
 
 
 def analyse(tr, bins=40, steps=0):

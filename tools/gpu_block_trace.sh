@@ -17,4 +17,5 @@ run() {
 run metric --bins 20 && \
 run c5 --spheres 4096 --march-steps 128 --views 1 --warm 2 --bins 20 && \
 run c5s --width 64 --height 64 --spheres 4096 --march-steps 128 --views 1 --warm 2 --bins 8 && \
-run c2 --width 256 --height 256 --spheres 64 --bins 20
+run c2 --width 256 --height 256 --spheres 64 --bins 20 && \
+run c3 --march-steps 64 --bins 20
