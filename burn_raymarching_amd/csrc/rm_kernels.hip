@@ -57,6 +57,9 @@
 #else
 #define RM_SCHED_BARRIER() ((void)0)
 #endif
+#ifndef RM_CYCLE_MAX
+#define RM_CYCLE_MAX 2  // longest period (2..4) the march's cycle exit detects (3, 4: no measurable gain)
+#endif
 #ifndef RM_ORDER_CLASSES
 #define RM_ORDER_CLASSES 16  // cost classes of the cost-ordered dispatch (order_append)
 #endif
@@ -1330,7 +1333,8 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   // fixed clamped), shader cycles inside the matrix-core steps, vector-path steps
   unsigned long long tr_paths = 0, tr_lse_cyc = 0, tr_vec = 0;
 #endif
-  auto soft_min_march = [&](const float p[3], bool fast, float Dprev) {
+  // choice: the step's wave-uniform choices, bit 0 unshifted, bit 1 fixed shift, bit 2 clamp-free
+  auto soft_min_march = [&](const float p[3], bool fast, float Dprev, int& choice) {
     bool none = shift_none_ok && __all(2.0f * fmaxf(Dprev, 0.0f) + a.lse_slack <= 90.0f * inv_kappa || gone);
     // or: the nearest sphere is no farther than sphere 0, k (rho_0 - r_0) = rho'_0 - k r_0 <= 90
     // bounds k d_min just as well (the first steps after the eye, where the 2 D bound is loose)
@@ -1338,6 +1342,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       none = __all(fixed_shift(p, kappa * kappa, Lds::v4(L.S0[0]), Lds::v4(L.S1[0])) - kr_first <= 90.0f || gone);
     float m = none ? 0.0f : -INFINITY, s = 0.0f;
     const bool fixed = !none && shift_fixed_ok && __all(psq(p) <= 1e10f || gone);
+    choice = (none ? 1 : 0) | (fixed ? 2 : 0) | (fast ? 4 : 0);
     if ((none || fixed) && a.mfma) {
       const float k2 = kappa * kappa;
       const int nrb = a.Mpad / 16;
@@ -1469,9 +1474,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     int st0 = 0;
 #ifdef RM_BLOCK_TRACE
     const unsigned long long tr_c_begin = __builtin_readcyclecounter();
-    float tr_cyc_t1 = __builtin_nanf(""), tr_cyc_t2 = __builtin_nanf(""), tr_cyc_d1 = __builtin_nanf(""),
-          tr_cyc_d2 = __builtin_nanf("");
-    int tr_cyc_first = -1;
+    unsigned long long tr_cyc = 0;  // period | step << 8 of the cycle exit
 #endif
     if constexpr (CAM) {
       // Camera mode: step 0 from the soft-min at the eye, evaluated once per view by the same
@@ -1493,9 +1496,16 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
         }
       }
     }
-    // march states (t, Dprev) one and two steps back (the cycle exit)
-    float cyc_t1 = __builtin_nanf(""), cyc_t2 = __builtin_nanf(""), cyc_d1 = __builtin_nanf(""),
-          cyc_d2 = __builtin_nanf("");
+    // the cycle exit's history: t one to four steps back, and the choices (3 bits per step,
+    // the latest in the low bits; 7 is no valid choice)
+    float cyc_t1 = __builtin_nanf(""), cyc_t2 = __builtin_nanf("");
+#if RM_CYCLE_MAX >= 3
+    float cyc_t3 = __builtin_nanf("");
+#endif
+#if RM_CYCLE_MAX >= 4
+    float cyc_t4 = __builtin_nanf("");
+#endif
+    int chist = 0xFFF;
     for (int st = st0; !dead && st < a.steps; ++st) {
 #if RM_PRIO_RAMP
       if (st == half) __builtin_amdgcn_s_setprio(2);
@@ -1505,45 +1515,67 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
         dead = true;
         break;
       }
-      // Cycle exit (exact): when every ray that is not gone repeats its march state (t, and the
-      // previous step's D, which the wave's choices depend on) of two steps earlier, the rest of
-      // the march repeats with period 2 (each step is a deterministic function of the wave's
-      // state; a ray cycling at a fixed distance cannot become gone later, the thresholds only
-      // grow), so the state after the last step is this one or the previous one by the parity of
-      // the steps left. Gone rays take their remaining bound steps here, as the march would.
-      if (a.early_exit && __all(gone || (t == cyc_t2 && Dprev == cyc_d2))) {
-        const int left = a.steps - st;
-        if (!gone && (left & 1)) {
-          t = cyc_t1;
-          Dprev = cyc_d1;
-          lb = Dprev - fabsf(Dprev);
-        }
-        if (gone)
-          for (int k = st; k < a.steps; ++k) {
-            const float q[3] = {fmaf(d[0], t, o[0]) - c0x, fmaf(d[1], t, o[1]) - c0y, fmaf(d[2], t, o[2]) - c0z};
-            t = fminf(t + (fsqrt(fmaf(q[2], q[2], fmaf(q[1], q[1], q[0] * q[0]))) - rprime), kTMax);
-          }
-        steps_saved += left;
-        break;
-      }
-      cyc_t2 = cyc_t1;
-      cyc_t1 = t;
-      cyc_d2 = cyc_d1;
-      cyc_d1 = Dprev;
-#ifdef RM_BLOCK_TRACE
-      // measurement: first step whose march state (t, D of the step before) repeats the state two
-      // steps earlier on every ray that is not gone (the march has entered a cycle of period <= 2)
-      if (tr_cyc_first < 0 && __all(gone || (t == tr_cyc_t2 && Dprev == tr_cyc_d2))) tr_cyc_first = st;
-      tr_cyc_t2 = tr_cyc_t1;
-      tr_cyc_t1 = t;
-      tr_cyc_d2 = tr_cyc_d1;
-      tr_cyc_d1 = Dprev;
-#endif
-      const float D = soft_min_march(p, all_safe(lb), Dprev);
+      int choice;
+      const float D = soft_min_march(p, all_safe(lb), Dprev, choice);
+      const float t_step = t;  // this step's state: (t_step, choice)
       t = fminf(t + (gone ? gone_step : D), kTMax);
       // next point: hard min >= soft-min D here, moved by |D|
       lb = D - fabsf(D);
       Dprev = D;
+      // Cycle exit (exact). A march step is a deterministic function of the wave's state: the t
+      // of every ray that is not gone and the step's wave-uniform choice (which carries all the
+      // previous step's D decides). When this step's state equals the state P steps back (P = 2,
+      // or up to RM_CYCLE_MAX) the march repeats with period P from there, so the state after
+      // the last step is the one (steps left) mod P steps after that earlier state. A ray cycling
+      // between fixed points cannot become gone later (its thresholds only grow); gone rays take
+      // their remaining bound steps here, as the march would. Of the last step's D the post-march
+      // needs only the clamp-free choice of the reconnect: the final state's choice bit 2.
+      if (a.early_exit && MODE != kRender) {
+        int P = 0;
+        if (choice == ((chist >> 3) & 7) && __all(gone || t_step == cyc_t2)) P = 2;
+#if RM_CYCLE_MAX >= 3
+        else if (choice == ((chist >> 6) & 7) && __all(gone || t_step == cyc_t3)) P = 3;
+#endif
+#if RM_CYCLE_MAX >= 4
+        else if (choice == ((chist >> 9) & 7) && __all(gone || t_step == cyc_t4)) P = 4;
+#endif
+        if (P != 0) {
+          // the state after the last step (step a.steps) is this step's state or the one `back`
+          // steps before it; `left` steps remain after this one
+          const int left = a.steps - 1 - st, m = a.steps - st, back = (P - m % P) % P;
+          const int cf = back == 0 ? choice : (chist >> (3 * (back - 1))) & 7;
+          if (!gone) {
+            if (back == 0) t = t_step;
+            else if (back == 1) t = cyc_t1;
+#if RM_CYCLE_MAX >= 3
+            else if (back == 2) t = cyc_t2;
+#endif
+#if RM_CYCLE_MAX >= 4
+            else if (back == 3) t = cyc_t3;
+#endif
+            lb = (cf & 4) ? INFINITY : -INFINITY;  // all_safe(lb) of the final state = its bit 2
+          } else {
+            for (int k = st + 1; k < a.steps; ++k) {
+              const float q[3] = {fmaf(d[0], t, o[0]) - c0x, fmaf(d[1], t, o[1]) - c0y, fmaf(d[2], t, o[2]) - c0z};
+              t = fminf(t + (fsqrt(fmaf(q[2], q[2], fmaf(q[1], q[1], q[0] * q[0]))) - rprime), kTMax);
+            }
+          }
+          steps_saved += left;
+#ifdef RM_BLOCK_TRACE
+          tr_cyc = (unsigned long long)P | ((unsigned long long)st << 8);
+#endif
+          break;
+        }
+#if RM_CYCLE_MAX >= 4
+        cyc_t4 = cyc_t3;
+#endif
+#if RM_CYCLE_MAX >= 3
+        cyc_t3 = cyc_t2;
+#endif
+        cyc_t2 = cyc_t1;
+        cyc_t1 = t_step;
+        chist = ((chist << 3) | choice) & 0xFFF;
+      }
     }
   RM_TRACE(4, __builtin_amdgcn_s_memrealtime());
   RM_TRACE(6, (unsigned long long)steps_saved);
@@ -1552,7 +1584,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   RM_TRACE(8, tr_lse_cyc);
   RM_TRACE(9, tr_vec);
   RM_TRACE(10, __builtin_readcyclecounter() - tr_c_begin);
-  RM_TRACE(11, (unsigned long long)(long long)tr_cyc_first);
+  RM_TRACE(11, tr_cyc);
 #endif
 #ifdef RM_LANE_STATS  // stats[3] += escaped lane-steps of the march + 5 sweeps per escaped lane of a live wave
     if (a.stats != nullptr && lane == 0)
