@@ -57,6 +57,9 @@
 #else
 #define RM_SCHED_BARRIER() ((void)0)
 #endif
+#ifndef RM_MARCH_BUFLOAD
+#define RM_MARCH_BUFLOAD 1  // matrix-core fragments by buffer loads (0: global loads)
+#endif
 #ifndef RM_CYCLE_MAX
 #define RM_CYCLE_MAX 2  // longest period (2..4) the march's cycle exit detects (3, 4: no measurable gain)
 #endif
@@ -79,6 +82,9 @@ constexpr int kMaxBlocksPerLaunch = 16384 * (256 / kBlock);
 constexpr int kSplitMinSpheres = 2048;
 #ifndef RM_SPLIT_WAVES
 #define RM_SPLIT_WAVES 4
+#endif
+#ifndef RM_SPLIT_MIN_WAVES
+#define RM_SPLIT_MIN_WAVES 4  // register budget of the split kernels (waves per SIMD; 5: 168 VGPR spills)
 #endif
 constexpr int kSplitWaves = RM_SPLIT_WAVES;  // waves per 64-ray block of the split march (2 or 4)
 static_assert(kSplitWaves == 2 || kSplitWaves == 4, "split blocks have 2 or 4 waves");
@@ -618,7 +624,7 @@ __device__ __forceinline__ void lse_point(const float p[3], const Lds& L, int np
 // (FIXED; w = 2^(k (r - r_0)), sh = the ray's own shift) for the lane's own ray -- the same sum
 // as lse_weighted up to fp32 rounding. xa / xb / xs: this wave's LDS exchange (64 uint4, 64
 // uint4, 64 floats).
-template <bool CLAMP, bool FIXED>
+template <bool CLAMP, bool FIXED, bool BUF = (RM_MARCH_BUFLOAD != 0)>
 __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, const uint4* __restrict__ At,
                                           const float* __restrict__ Wt, int nrb, uint4* xa, uint4* xb, float* xs,
                                           int lane) {
@@ -652,9 +658,22 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
     __builtin_amdgcn_wave_barrier();
     return 0.0f;
   }
+  // BUF: buffer loads -- the row block's byte offset in a scalar register, the lane's offset
+  // fixed in a vector register, no per-load 64-bit address arithmetic on the vector units (the
+  // unsplit march: +3 %); else global loads (the split march, where buffer loads measured slower)
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)At, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Wt + (FIXED ? 16 : 0)), (short)0, 0x7fffffff, 0x00020000);
+  const int va = lane * 16, vw = g * 16;
   const float* wsrc = Wt + (FIXED ? 16 : 0) + 4 * g;
-  auto load_a = [&](int rb) { return __builtin_bit_cast(bf16x8, At[rb * 64 + lane]); };
-  auto load_w = [&](int rb) { return *reinterpret_cast<const float4*>(wsrc + rb * 32); };
+  auto load_a = [&](int rb) {
+    if constexpr (BUF) return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, va, rb * 1024, 0));
+    else return __builtin_bit_cast(bf16x8, At[rb * 64 + lane]);
+  };
+  auto load_w = [&](int rb) {
+    if constexpr (BUF) return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw, vw, rb * 128, 0));
+    else return *reinterpret_cast<const float4*>(wsrc + rb * 32);
+  };
   auto tile = [&](const bf16x8& A, f32x4 (&D)[4]) {
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) D[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[cb], zero, 0, 0, 0);
@@ -734,7 +753,7 @@ __device__ __forceinline__ float lse_mfma_quarters(const float p[3], float k2, f
 // A march step's soft-min D at p on the matrix cores without a shift (soft_min_march's
 // unshifted step; shared with write_origins like march_d_fixed). comb != nullptr: a split
 // block's wave, At / Wt / nrb its quarter (split_combine); quarters: all quarters in one wave.
-template <bool CLAMP>
+template <bool CLAMP, bool BUF = (RM_MARCH_BUFLOAD != 0)>
 __device__ __forceinline__ float march_d_none(const float p[3], float kappa, float inv_kappa,
                                               const uint4* __restrict__ At, const float* __restrict__ Wt, int nrb,
                                               uint4* xa, uint4* xb, float* xs, int lane, float* comb = nullptr,
@@ -744,7 +763,7 @@ __device__ __forceinline__ float march_d_none(const float p[3], float kappa, flo
   if (quarters) {
     s = lse_mfma_quarters<CLAMP, false>(p, kappa * kappa, 0.0f, At, Wt, nrb, xa, xb, xs, lane);
   } else {
-    s = lse_mfma<CLAMP, false>(p, kappa * kappa, 0.0f, At, Wt, nrb, xa, xb, xs, lane);
+    s = lse_mfma<CLAMP, false, BUF>(p, kappa * kappa, 0.0f, At, Wt, nrb, xa, xb, xs, lane);
     if (comb != nullptr) s = split_combine(s, comb, wave, lane);
   }
   return -flog2(fmaxf(s, 1e-30f)) * inv_kappa;
@@ -761,7 +780,7 @@ __device__ __forceinline__ float fixed_shift(const float p[3], float k2, const f
 // A march step's soft-min D at p on the matrix cores with the fixed shift sh = rho'_0 (sphere 0;
 // S00 / S10 = its records S0[0] / S1[0]) -- soft_min_march's fixed-shift step, shared with the
 // per-view origin step (write_origins) so that both give the same bits.
-template <bool CLAMP>
+template <bool CLAMP, bool BUF = (RM_MARCH_BUFLOAD != 0)>
 __device__ __forceinline__ float march_d_fixed(const float p[3], float kappa, float inv_kappa, float kr_first,
                                                const float4& S00, const float4& S10, const uint4* __restrict__ At,
                                                const float* __restrict__ Wt, int nrb, uint4* xa, uint4* xb,
@@ -774,7 +793,7 @@ __device__ __forceinline__ float march_d_fixed(const float p[3], float kappa, fl
   if (quarters) {
     s = lse_mfma_quarters<CLAMP, true>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
   } else {
-    s = lse_mfma<CLAMP, true>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
+    s = lse_mfma<CLAMP, true, BUF>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
     if (comb != nullptr) s = split_combine(s, comb, wave, lane);
   }
   const float m = kr_first - sh;
@@ -1222,7 +1241,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a);
 // a.btrace[kTraceWords * (blockIdx.x * kWaves + wave) ...] (tools/block_trace.py).
 // SPLIT: the split march (RM_MARCH_SPLIT, KArgs::split).
 template <int MODE, bool CAM, bool SPLIT>
-__global__ __launch_bounds__(kBlock, kMinWavesPerSimd) void rm_ray_kernel(const KArgs a) {
+__global__ __launch_bounds__(kBlock, SPLIT ? RM_SPLIT_MIN_WAVES : kMinWavesPerSimd) void rm_ray_kernel(const KArgs a) {
 #ifdef RM_BLOCK_TRACE
   const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
   ray_body<MODE, CAM, SPLIT>(a);
@@ -1354,6 +1373,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       tr_paths += 1ull << (16 * ((fixed ? 2 : 0) + (fast ? 0 : 1)));
 #endif
       float Dm;
+      constexpr bool kBuf = RM_MARCH_BUFLOAD != 0 && !SPLIT;  // split: global loads (measured faster)
       const uint4* At = L.At;
       const float* Wt = L.Wt;
       int nq = nrb;
@@ -1367,11 +1387,11 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       }
       if (fixed) {  // the ray's shift: rho'_0 of sphere 0 (any value near it keeps +-100 headroom)
         const float4 A = Lds::v4(L.S0[0]), B = Lds::v4(L.S1[0]);
-        Dm = fast ? march_d_fixed<false>(p, kappa, inv_kappa, kr_first, A, B, At, Wt, nq, xa, xb, xs, lane, comb, wave)
-                  : march_d_fixed<true>(p, kappa, inv_kappa, kr_first, A, B, At, Wt, nq, xa, xb, xs, lane, comb, wave);
+        Dm = fast ? march_d_fixed<false, kBuf>(p, kappa, inv_kappa, kr_first, A, B, At, Wt, nq, xa, xb, xs, lane, comb, wave)
+                  : march_d_fixed<true, kBuf>(p, kappa, inv_kappa, kr_first, A, B, At, Wt, nq, xa, xb, xs, lane, comb, wave);
       } else {
-        Dm = fast ? march_d_none<false>(p, kappa, inv_kappa, At, Wt, nq, xa, xb, xs, lane, comb, wave)
-                  : march_d_none<true>(p, kappa, inv_kappa, At, Wt, nq, xa, xb, xs, lane, comb, wave);
+        Dm = fast ? march_d_none<false, kBuf>(p, kappa, inv_kappa, At, Wt, nq, xa, xb, xs, lane, comb, wave)
+                  : march_d_none<true, kBuf>(p, kappa, inv_kappa, At, Wt, nq, xa, xb, xs, lane, comb, wave);
       }
       (void)k2;
 #ifdef RM_BLOCK_TRACE

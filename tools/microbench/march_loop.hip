@@ -11,6 +11,8 @@
 //   2 loads + MFMA only (no sqrt / exp consume)
 //   3 loads four row blocks ahead (a ring of four register slots, explicit waits)
 //   4 fragments from LDS (nrb <= 64; staged once)
+//   5 v_mfma_f32_32x32x16_bf16 tiles (2 K halves x 2 ray tiles per 32 spheres) instead of
+//     16x16x32: half the MFMA issue per (sphere, ray) value
 // and prints cycles per row block per wave (s_memtime) and wall time.
 //
 // Build: hipcc --offload-arch=gfx950 -O3 march_loop.hip -o march_loop ; run: ./march_loop [nrb] [steps]
@@ -77,10 +79,44 @@ __global__ __launch_bounds__(256) void march_loop(const uint4* __restrict__ At, 
       }
     }
   };
+  typedef float f32x16 __attribute__((ext_vector_type(16)));
   long long t0 = __builtin_readcyclecounter();
   for (int st = 0; st < steps; ++st) {
     f32x4 D[4];
-    if constexpr (VAR == 1) {
+    if constexpr (VAR == 5) {
+      // 32x32x16 tiles: per 32-sphere block two K halves x two 32-ray column tiles; a lane holds
+      // 16 values per column tile (the same sqrt / exp / fma per value as the 16x16x32 loop)
+      const f32x16 z16 = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f,
+                          0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+      float acc2[2] = {0.0f, 0.0f};
+      bf16x8 A0 = load_a(0), A1 = load_a(1);
+      float4 wv4[4];
+      for (int rb = 0; rb < nrb; rb += 2) {  // one 32-sphere block = two 16-sphere row blocks of data
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          f32x16 Dv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B[2 * c], z16, 0, 0, 0);
+          Dv = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B[2 * c + 1], Dv, 0, 0, 0);
+          if (c == 0) {
+            const int rn = min(rb + 2, nrb - 2);
+            A0 = load_a(rn);
+            A1 = load_a(rn + 1);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) wv4[u] = load_w(rb + (u >> 1));
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float4 w4 = wv4[r >> 2];
+            const float wr = (r & 3) == 0 ? w4.x : ((r & 3) == 1 ? w4.y : ((r & 3) == 2 ? w4.z : w4.w));
+            const float rho = __builtin_amdgcn_sqrtf(qclamp(Dv[r], QMIN));
+            acc2[c] = fmaf(wr, __builtin_amdgcn_exp2f(-rho), acc2[c]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+      acc[0] += acc2[0];
+      acc[1] += acc2[1];
+    } else if constexpr (VAR == 1) {
       const bf16x8 A = load_a(st & 1);
       const float4 w = load_w(st & 1);
       for (int rb = 0; rb < nrb; ++rb) {
@@ -187,6 +223,7 @@ int main(int argc, char** argv) {
     run<2>(At, Wt, nrb, steps, out, cyc, blocks, threads);
     run<3>(At, Wt, nrb, steps, out, cyc, blocks, threads);
     if (nrb <= 64) run<4>(At, Wt, nrb, steps, out, cyc, blocks, threads);
+    run<5>(At, Wt, nrb, steps, out, cyc, blocks, threads);
   }
   return 0;
 }
