@@ -250,6 +250,7 @@ def main():
         ev[j][0].record()
         step(i)
         ev[j][1].record()
+    host_s = time.perf_counter() - t0  # host time to submit the K steps (before the final sync)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -326,7 +327,7 @@ def main():
     pmc, pmc_src = _latest_profile("r*_pmc_sq.json", key, "train_kernel")
     alg_bytes = rays_per_rank * BYTES_PER_RAY_CAMERA
     mpad = (M + 31) // 32 * 32
-    slab_bytes = (rays_per_rank + 255) // 256 * (mpad * 12 + 8) * 4  # partial-gradient slabs, if all written
+    slab_bytes = (rays_per_rank + 255) // 256 * (mpad * 8 + 8) * 4  # partial-gradient slabs, if all written
     canonical = None
     if canon_ms:
         ach = flop_per_ray * rays_per_rank / (canon_ms * 1e-3) / 1e12
@@ -389,6 +390,7 @@ def main():
                        "parallelism": f"views-dp{world}"},
             "value_median": round(rays_global / (med_ms * 1e-3) / 1e6, 3),
             "ms_per_step_median": round(med_ms, 4),
+            "host_submit_ms_per_step": round(host_s / args.steps * 1e3, 4),
             "ms_per_step_min_max": [round(float(step_ms.min()), 4), round(float(step_ms.max()), 4)],
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -63,6 +63,9 @@
 #ifndef RM_CYCLE_MAX
 #define RM_CYCLE_MAX 2  // longest period (2..4) the march's cycle exit detects (3, 4: no measurable gain)
 #endif
+#ifndef RM_HEAVY_PRIO
+#define RM_HEAVY_PRIO 0  // s_setprio(2) for the blocks of the RM_HEAVY_PRIO dearest cost classes
+#endif
 #ifndef RM_ORDER_CLASSES
 #define RM_ORDER_CLASSES 16  // cost classes of the cost-ordered dispatch (order_append)
 #endif
@@ -1094,7 +1097,7 @@ __device__ __forceinline__ bool escapes(const float o[3], const float d[3], floa
 // rays that march all their steps -- first, the cheap border tiles last, where they fill the
 // machine while the heavy blocks finish. Partials stay indexed by the logical block, so the
 // gradient sums (and every result) do not depend on the order.
-__device__ __forceinline__ long long ray_block(const KArgs& a) {
+__device__ __forceinline__ long long ray_block(const KArgs& a, int* cls = nullptr) {
   int b = blockIdx.x;
   if (a.block_order == nullptr) return b;
   // The dispatcher hands block i to XCD i % 8. With the views interleaved (b = rank * V + v),
@@ -1122,7 +1125,10 @@ __device__ __forceinline__ long long ray_block(const KArgs& a) {
       }
       tot += n;
     }
-    if (tot == (int)gridDim.x && cb >= 0) return a.olist_r[cb * kMaxBlocksPerLaunch + (b - base)];
+    if (tot == (int)gridDim.x && cb >= 0) {
+      if (cls != nullptr) *cls = cb;
+      return a.olist_r[cb * kMaxBlocksPerLaunch + (b - base)];
+    }
   }
   const int r = b / a.order_views, v = b - r * a.order_views;
   return (long long)v * a.order_tiles + a.block_order[r];
@@ -1168,7 +1174,7 @@ __device__ __forceinline__ void escaped_block(const KArgs& a, const Lds& L, long
     float acc = L.slots[tid];
 #pragma unroll
     for (int w = 1; w < kWaves; ++w) acc += L.slots[w * 8 + tid];
-    rec[(long long)a.Mpad * 12 + tid] = acc;
+    rec[(long long)a.Mpad * 8 + tid] = acc;
   }
 }
 
@@ -1287,8 +1293,14 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   L.misc = L.slots + kSlotBytes / sizeof(float);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const long long blk = ray_block(a);
+  int cls = -1;  // the block's cost class in the previous launch (cost-ordered dispatch), else -1
+  const long long blk = ray_block(a, &cls);
   const long long li = SPLIT ? blk * 64 + lane : blk * kBlock + tid;
+#if RM_HEAVY_PRIO
+  // the dearest class's waves first at the SIMD's issue arbiter: they set the launch's critical
+  // path, the cheaper waves fill the issue slots they leave
+  if (cls >= 0 && cls < RM_HEAVY_PRIO) __builtin_amdgcn_s_setprio(2);
+#endif
   const bool valid = li < a.n_rays;
   long long ri = a.ray_begin + (valid ? li : 0);  // becomes the ray's row in the [N,3] tensors
   // the wave that writes this ray's outputs and runs its post-march forward and backward
@@ -1839,7 +1851,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
         float acc = wscal[lane];
 #pragma unroll
         for (int w = 1; w < (SPLIT ? kSplitWaves : kWaves); ++w) acc += wscal[w * 8 + lane];
-        rec[(long long)a.Mpad * 12 + lane] = acc;
+        rec[(long long)a.Mpad * 8 + lane] = acc;
       }
     }
     return;
@@ -1887,7 +1899,9 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     const float2* R2 = reinterpret_cast<const float2*>(R4 + 7 * (size_t)np);
     const int ngrp = (a.Mpad + 63) / 64;
     // the block's live waves sum their per-sphere lane sums in wave order into the record
-    auto combine = [&](const float (&v)[8], int ncomp, long long rec_base, int grp) {
+    // ncomp = 8: sweep 1 writes the sphere's 8 columns; ncomp = 4: sweep 2 adds its (gc, gr)
+    // terms to columns 0-3 (written by sweep 1 of this block before the barrier between the sweeps)
+    auto combine = [&](const float (&v)[8], int ncomp, int grp) {
       float* cb = comb + (RM_BWD_COMB_BUFS > 1 ? (chunk_ctr & 1) * (kWaves * 8 * 64) : 0);
 #pragma unroll
       for (int c = 0; c < 8; ++c)
@@ -1895,7 +1909,11 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       __syncthreads();
       for (int e = atid; e < 64 * ncomp; e += astride) {
         const int sl = e / ncomp, c = e - sl * ncomp;
-        if (grp * 64 + sl < a.Mpad) rec[rec_base + (long long)(grp * 64 + sl) * ncomp + c] = live_sum(cb + c * 64 + sl, 8 * 64);
+        if (grp * 64 + sl < a.Mpad) {
+          float* dst = rec + (long long)(grp * 64 + sl) * 8 + c;
+          const float sum = live_sum(cb + c * 64 + sl, 8 * 64);
+          *dst = ncomp == 8 ? sum : *dst + sum;
+        }
       }
       if (RM_BWD_COMB_BUFS == 1) __syncthreads();  // one buffer: read by every live wave before reuse
       ++chunk_ctr;
@@ -1995,7 +2013,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
           }
           const float v[8] = {agc[0].x + agc[0].y, agc[1].x + agc[1].y, agc[2].x + agc[2].y, agr.x + agr.y,
                               acol[0].x + acol[0].y, acol[1].x + acol[1].y, acol[2].x + acol[2].y, 0.0f};
-          combine(v, 8, 0, grp);
+          combine(v, 8, grp);
         }
       };
       if (fast_f) sweep1(std::false_type{});
@@ -2062,7 +2080,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
           }
           const float v[8] = {agc[0].x + agc[0].y, agc[1].x + agc[1].y, agc[2].x + agc[2].y, agr.x + agr.y,
                               0.0f, 0.0f, 0.0f, 0.0f};
-          combine(v, 4, (long long)a.Mpad * 8, grp);
+          combine(v, 4, grp);
         }
       };
       if (fast_a) sweep2(std::false_type{});
@@ -2168,8 +2186,10 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
           }
         }
         __syncthreads();
-        for (int e = atid; e < kChunkBwd * 4; e += astride)
-          rec[(long long)a.Mpad * 8 + (long long)(t0 + jc) * 4 + e] = live_sum(sb + e, kChunkBwd * 4);
+        for (int e = atid; e < kChunkBwd * 4; e += astride) {  // added to sweep 1's columns 0-3
+          float* dst = rec + (long long)(t0 + jc + (e >> 2)) * 8 + (e & 3);
+          *dst += live_sum(sb + e, kChunkBwd * 4);
+        }
       }
     };
     if (fast_a)
@@ -2186,20 +2206,21 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     float acc = wscal[lane];
 #pragma unroll
     for (int w = 1; w < (SPLIT ? kSplitWaves : kWaves); ++w) acc += wscal[w * 8 + lane];
-    rec[(long long)a.Mpad * 12 + lane] = lane == 7 ? 1.0f : acc;  // scalar 7: live flag
+    rec[(long long)a.Mpad * 8 + lane] = lane == 7 ? 1.0f : acc;  // scalar 7: live flag
   }
 }
 
 // ---- cross-block reduction (fixed order => deterministic) --------------------------------
-// Partial record of one ray block (rec = Mpad*12 + 8 floats):
-//   [Mpad][8] sweep 1 (gc.xyz, gr, gcol.rgb, 0) | [Mpad][4] sweep 2 (gc.xyz, gr) | 8 scalars
+// Partial record of one ray block (rec = Mpad*8 + 8 floats):
+//   [Mpad][8] (gc.xyz, gr, gcol.rgb, 0) -- backward sweep 1's terms, sweep 2's (gc, gr) terms added
+//   by the block itself -- | 8 scalars
 // Scalar 7 is the block's live flag: 0 when every wave of the block left the march early (its
 // per-sphere columns are all zero and were not written), 1 otherwise.
 // Output columns (ncols = Mpad*8 + 8): [Mpad][8] combined per-sphere grads | 8 scalars.
 //
 // Pass 1, grid (column blocks x segments of ray blocks): each block sums its segment for its 256
-// columns into S[seg][col] -- one addition chain per column in ray-block order (sweep-2 terms
-// added right after their row's sweep-1 term), loads batched eight rows at a time. Rows of dead
+// columns into S[seg][col] -- one addition chain per column in ray-block order, loads batched
+// eight rows at a time. Rows of dead
 // blocks are skipped: they only hold zeros, and adding +0 leaves a chain unchanged, so the sums
 // are those of the full chain.
 struct FinalArgs {
@@ -2223,7 +2244,7 @@ __global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restric
   // rows of this segment to visit, in order: every row for the scalars, live rows otherwise
   {
     const int b = b0 + tid;
-    const bool take = b < b1 && (scalars || P[(long long)b * rec + (long long)Mpad * 12 + 7] != 0.0f);
+    const bool take = b < b1 && (scalars || P[(long long)b * rec + (long long)Mpad * 8 + 7] != 0.0f);
     const unsigned long long m = __ballot(take);
     if (lane == 0) wcount[wave] = __popcll(m);
     __syncthreads();
@@ -2234,30 +2255,14 @@ __global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restric
   }
   const int nrows = wcount[0] + wcount[1] + wcount[2] + wcount[3];
   if (col < ncols) {
-    long long c1, c2 = -1;
-    if (col < Mpad * 8) {
-      c1 = col;
-      const int j = col >> 3, comp = col & 7;
-      if (comp < 4) c2 = (long long)Mpad * 8 + (long long)j * 4 + comp;
-    } else {
-      c1 = (long long)Mpad * 12 + (col - Mpad * 8);
-    }
-    float acc = 0.0f;
+    float acc = 0.0f;  // columns map 1:1 onto the record (per-sphere block, then the scalars)
     for (int i0 = 0; i0 < nrows; i0 += kReduceBatch) {
-      float v1[kReduceBatch], v2[kReduceBatch];
+      float v1[kReduceBatch];
 #pragma unroll
-      for (int u = 0; u < kReduceBatch; ++u) {
-        const int i = min(i0 + u, nrows - 1);
-        const float* r = P + (long long)rows[i] * rec;
-        v1[u] = r[c1];
-        v2[u] = c2 >= 0 ? r[c2] : 0.0f;
-      }
+      for (int u = 0; u < kReduceBatch; ++u) v1[u] = P[(long long)rows[min(i0 + u, nrows - 1)] * rec + col];
 #pragma unroll
       for (int u = 0; u < kReduceBatch; ++u)
-        if (i0 + u < nrows) {
-          acc += v1[u];
-          if (c2 >= 0) acc += v2[u];
-        }
+        if (i0 + u < nrows) acc += v1[u];
     }
     S[(long long)blockIdx.y * ncols + col] = acc;
   }
@@ -2269,32 +2274,41 @@ __global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restric
 // gld = (g_ell - ldn (ldn . g_ell)) / |ld| applies the Jacobian of ld / |ld| (renderer_diff.rs:49-50).
 __global__ __launch_bounds__(256) void rm_finalize_grads(const float* __restrict__ S, int nseg, int M, int Mpad,
                                                          FinalArgs f) {
+  // 64 columns per block, four threads per column: thread (chain k, column) sums the segments
+  // s = k mod 4 in order -- the four chains of one thread's former loop (a[s & 3] += v[s]) --
+  // and the chains are combined as before, (a0 + a1) + (a2 + a3): the same bits, the loads
+  // spread over four times as many CUs
+  __shared__ float part[4][64];
   const int ncols = Mpad * 8 + 8;
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  (void)nseg;  // == kReduceSegs always (pass 1 writes every segment, empty ones as 0): all loads in
-  // flight, then four chains s mod 4 combined in a fixed order
-  auto seg_sum = [&](int c) {
-    float v[kReduceSegs];
+  const int cl = threadIdx.x & 63, chain = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + cl;
+  (void)nseg;  // == kReduceSegs always (pass 1 writes every segment, empty ones as 0)
+  static_assert(kReduceSegs % 4 == 0, "four chains");
+  {
+    float v[kReduceSegs / 4];
+    const int c = min(col, ncols - 1);
 #pragma unroll
-    for (int s = 0; s < kReduceSegs; ++s) v[s] = S[(long long)s * ncols + c];
-    float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int u = 0; u < kReduceSegs / 4; ++u) v[u] = S[(long long)(4 * u + chain) * ncols + c];
+    float acc = 0.0f;
 #pragma unroll
-    for (int s = 0; s < kReduceSegs; ++s) a[s & 3] += v[s];
-    return (a[0] + a[1]) + (a[2] + a[3]);
-  };
-  if (col >= ncols) return;
+    for (int u = 0; u < kReduceSegs / 4; ++u) acc += v[u];
+    part[chain][cl] = acc;
+  }
+  __syncthreads();
+  if (chain != 0 || col >= ncols) return;
+  auto seg_sum = [&](int l) { return (part[0][l] + part[1][l]) + (part[2][l] + part[3][l]); };
   if (col < Mpad * 8) {
     const int j = col >> 3, comp = col & 7;
     if (j >= M || comp == 7) return;
-    const float v = seg_sum(col);
+    const float v = seg_sum(cl);
     float* dst = comp < 3 ? (f.gc ? f.gc + 3 * j + comp : nullptr)
                           : (comp == 3 ? (f.gr ? f.gr + j : nullptr) : (f.gcol ? f.gcol + 3 * j + (comp - 4) : nullptr));
     if (dst) *dst = f.accumulate ? *dst + v : v;
     return;
   }
-  const int sc = col - Mpad * 8;
+  const int sc = col - Mpad * 8;  // Mpad * 8 is a multiple of 64: the scalars open their block
   if (sc == 0 && f.gld) {
-    const float r0 = seg_sum(col), r1 = seg_sum(col + 1), r2 = seg_sum(col + 2);
+    const float r0 = seg_sum(cl), r1 = seg_sum(cl + 1), r2 = seg_sum(cl + 2);
     const float l0 = f.light_dir[0], l1 = f.light_dir[1], l2 = f.light_dir[2];
     const float len = sqrtf(l0 * l0 + l1 * l1 + l2 * l2);
     const float ln[3] = {l0 / len, l1 / len, l2 / len};
@@ -2306,10 +2320,10 @@ __global__ __launch_bounds__(256) void rm_finalize_grads(const float* __restrict
       f.gld[c] = f.accumulate ? f.gld[c] + gv : gv;
     }
   } else if (sc == 3 && f.gamb) {
-    const float v = seg_sum(col);
+    const float v = seg_sum(cl);
     f.gamb[0] = f.accumulate ? f.gamb[0] + v : v;
   } else if (sc == 4 && f.loss_sum) {
-    const float v = seg_sum(col);
+    const float v = seg_sum(cl);
     f.loss_sum[0] = f.accumulate ? f.loss_sum[0] + v : v;
   }
 }
@@ -2619,7 +2633,7 @@ long long max_blocks_per_launch() {
   return (v >= 1 && v <= kMaxBlocksPerLaunch) ? v : kMaxBlocksPerLaunch;
 }
 
-long long rec_floats(int Mpad) { return (long long)Mpad * 12 + 8; }
+long long rec_floats(int Mpad) { return (long long)Mpad * 8 + 8; }
 
 size_t ws_need(long long max_rays, int M, int rays_per_block = kBlock) {
   const int Mpad = pad_spheres(M);
@@ -2919,8 +2933,12 @@ int run(rm_context* ctx, const Call& c) {
     // cost-ordered dispatch from the previous launch over the same views (single-launch calls)
     const bool has_rec = c.mode == kBwd || c.mode == kTrain;
     unsigned long long key = 0;
+    static const bool env_static = [] {  // RM_STATIC_ORDER=1: as RM_MARCH_STATIC_ORDER (A/B runs)
+      const char* e = std::getenv("RM_STATIC_ORDER");
+      return e != nullptr && e[0] == '1';
+    }();
     if (a.block_order != nullptr && has_rec && nb == blocks_left && done == 0 &&
-        (c.march->flags & RM_MARCH_STATIC_ORDER) == 0) {
+        (c.march->flags & RM_MARCH_STATIC_ORDER) == 0 && !env_static) {
       key = ((unsigned long long)c.W << 48) ^ ((unsigned long long)c.H << 32) ^ ((unsigned long long)c.views << 24) ^
             ((unsigned long long)Mpad << 1) ^ 1ull ^ ((unsigned long long)split << 2);
       constexpr int kCls = RM_ORDER_CLASSES;
@@ -3004,7 +3022,8 @@ int run(rm_context* ctx, const Call& c) {
       hipLaunchKernelGGL(rm_reduce_partials, dim3((unsigned)xblocks, (unsigned)segs), dim3(256), 0, ctx->stream, P,
                          a.rec, M, Mpad, nblocks, seg_len, S);
       RM_HIP(ctx, hipGetLastError());
-      hipLaunchKernelGGL(rm_finalize_grads, dim3((unsigned)xblocks), dim3(256), 0, ctx->stream, S, segs, M, Mpad, fa);
+      hipLaunchKernelGGL(rm_finalize_grads, dim3((unsigned)((ncols + 63) / 64)), dim3(256), 0, ctx->stream, S, segs, M,
+                         Mpad, fa);
       RM_HIP(ctx, hipGetLastError());
     }
     done += nr;

@@ -15,6 +15,8 @@ for r in $(seq 1 $ROUNDS); do
         c5) args="--spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 4 --warmup 2" ;;
         c3) args="--march-steps 64 --steps 10" ;;
         c4) args="--width 1024 --height 1024 --spheres 1024 --march-steps 64 --views-per-gpu 4 --steps 4 --warmup 2" ;;
+        c5r1) args="--spheres 4096 --march-steps 128 --views-per-gpu 1 --ring 1 --steps 4 --warmup 2" ;;
+        c5w) args="--spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 4 --warmup 12" ;;
         c5s) args="--width 64 --height 64 --spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 4 --warmup 2" ;;
       esac
       timeout -k 10 200 python bench.py --cpu-baseline off $args > gpurun_out/ab/${c}_${lib}_$r.json || exit 1
