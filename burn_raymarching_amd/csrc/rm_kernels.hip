@@ -148,7 +148,7 @@ struct KArgs {
   float progress, inv_count;
   float light_fixed[3];  // kRender: renderer.rs:27-32 light, normalised on the host in f32
   float* dbg;       // optional per-ray intermediates [n][16] (diagnostics; see rm_debug_intermediates)
-  float* partials;  // [gridDim.x][rec], rec = Mpad*12 + 8
+  float* partials;  // [gridDim.x][rec], rec = Mpad*8 + 8
   long long rec;
 #ifdef RM_BLOCK_TRACE
   unsigned long long* btrace;  // measurement build: per-wave timing records (rm_ray_kernel)
@@ -526,8 +526,11 @@ __global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, float* __re
 
 // The per-view origin steps (write_origins), one 64-thread block (one wave) per view, after the
 // records are complete: the views run on separate CUs side by side.
-__global__ __launch_bounds__(64) void rm_origin_kernel(const KArgs a, const float4* __restrict__ rec, int nprep) {
-  __shared__ __attribute__((aligned(16))) unsigned char xch[64 * 36];
+// A split launch's origin step runs its four quarters on four waves of the block (the split
+// march's own combine, same order as lse_mfma_quarters: the same bits).
+constexpr int kOriginXch = 64 * 36;  // bytes of march exchange per wave
+__global__ __launch_bounds__(256) void rm_origin_kernel(const KArgs a, const float4* __restrict__ rec, int nprep) {
+  __shared__ __attribute__((aligned(16))) unsigned char xch[kSplitWaves * kOriginXch + kSplitWaves * 64 * 4];
   const int np = a.Mpad / 2;
   const uint4* At = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(rec) + tiles_offset(np, nprep));
   const float* Wt = reinterpret_cast<const float*>(At + (size_t)(np / 8) * 64);
@@ -819,22 +822,37 @@ __device__ void write_origins(const KArgs& a, const float4& S00, const float4& S
   const bool shift_fixed_ok = kappa * (rmax + spread) * 1.001f <= 100.0f;
   const bool shift_none_ok = kappa * rmax * 1.001f <= 30.0f;
   const float kr_first = kappa * a.radius[0];
-  uint4* xa = reinterpret_cast<uint4*>(xch);
-  uint4* xb = reinterpret_cast<uint4*>(xch) + 64;
-  float* xs = reinterpret_cast<float*>(xch) + 64 * 8;
+  // a split launch with a block of kSplitWaves waves: wave w sums quarter w, combined in wave
+  // order (split_combine); one wave alone sums the quarters in turn (lse_mfma_quarters)
+  const bool par = a.split != 0 && (int)blockDim.x == 64 * kSplitWaves;
+  const int wave = par ? (int)(threadIdx.x >> 6) : 0;
+  uint4* xa = reinterpret_cast<uint4*>(xch + wave * kOriginXch);
+  uint4* xb = xa + 64;
+  float* xs = reinterpret_cast<float*>(xa) + 64 * 8;
+  float* comb = par ? reinterpret_cast<float*>(xch + kSplitWaves * kOriginXch) : nullptr;
+  const int nrb = np / 8;
+  const uint4* Aq = At;
+  const float* Wq = Wt;
+  int nq = nrb;
+  if (par) {
+    const int r0 = part_rb(nrb, wave);
+    nq = part_rb(nrb, wave + 1) - r0;
+    Aq += (size_t)r0 * 64;
+    Wq += (size_t)r0 * 32;
+  }
   {
     const float p[3] = {a.cams[v].eye[0], a.cams[v].eye[1], a.cams[v].eye[2]};
     float D = __builtin_nanf("");
     // the first step's choice in soft_min_march: unshifted when sphere 0 proves it safe, else
-    // the fixed shift (else the vector path: not shared)
+    // the fixed shift (else the vector path: not shared); block-uniform
     const bool none = a.mfma && shift_none_ok && fixed_shift(p, kappa * kappa, S00, S10) - kr_first <= 90.0f;
     // (a split launch's first step adds the four quarters' sums: the same here)
     if (none)
-      D = march_d_none<true>(p, kappa, inv_kappa, At, Wt, np / 8, xa, xb, xs, lane, nullptr, 0, a.split != 0);
+      D = march_d_none<true>(p, kappa, inv_kappa, Aq, Wq, nq, xa, xb, xs, lane, comb, wave, a.split != 0 && !par);
     else if (a.mfma && shift_fixed_ok && psq(p) <= 1e10f)
-      D = march_d_fixed<true>(p, kappa, inv_kappa, kr_first, S00, S10, At, Wt, np / 8, xa, xb, xs, lane, nullptr, 0,
-                              a.split != 0);
-    if (lane == 0) orig[v] = D;
+      D = march_d_fixed<true>(p, kappa, inv_kappa, kr_first, S00, S10, Aq, Wq, nq, xa, xb, xs, lane, comb, wave,
+                              a.split != 0 && !par);
+    if (lane == 0 && wave == 0) orig[v] = D;
   }
 }
 
@@ -2394,11 +2412,13 @@ __device__ __forceinline__ void repulsion_row(const float* c, int M, int s, int 
   for (int j = j0; j < M; j += stride) {
     const float ox = c[3 * j], oy = c[3 * j + 1], oz = c[3 * j + 2];
     const float q = (csq + (ox * ox + oy * oy + oz * oz)) - (cx * ox + cy * oy + cz * oz) * 2.0f;
-    const float rho = sqrtf(fmaxf(q, 1e-6f));
+    const float qc = fmaxf(q, 1e-6f);
+    const float rho = sqrtf(qc);
     const float den = rho + (j == s ? 100.0f : 0.0f) + 1e-6f;
-    v[3] += 1.0f / den;
+    const float inv = frcp(den);  // v_rcp / v_rsq (1 ulp) instead of IEEE divisions: O(M^2) pairs
+    v[3] += inv;
     if (j != s && q >= 1e-6f) {  // clamp_min(1e-6) gate (the diagonal has q ~ 0)
-      const float gs = -2.0f / (den * den) / rho;
+      const float gs = -2.0f * inv * inv * frsq(qc);
       v[0] += gs * (cx - ox);
       v[1] += gs * (cy - oy);
       v[2] += gs * (cz - oz);
@@ -2886,7 +2906,8 @@ int run(rm_context* ctx, const Call& c) {
       RM_HIP(ctx, hipGetLastError());
     }
     if (a.origin != nullptr) {
-      hipLaunchKernelGGL(rm_origin_kernel, dim3(c.views), dim3(64), 0, ctx->stream, a, (const float4*)ctx->rec, nprep);
+      hipLaunchKernelGGL(rm_origin_kernel, dim3(c.views), dim3(a.split ? 64 * kSplitWaves : 64), 0, ctx->stream, a,
+                         (const float4*)ctx->rec, nprep);
       RM_HIP(ctx, hipGetLastError());
     }
     a.rec_buf = (const float4*)ctx->rec;
