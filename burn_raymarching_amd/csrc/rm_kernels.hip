@@ -226,6 +226,19 @@ struct Lds {  // the sphere records (global, scalar-loaded) plus the kernel's LD
     const f4v v = P2[i];
     return make_float2(v.x, v.y);
   }
+  // the same records from pair `off` on (a split block's quarter of the vector sweeps)
+  __device__ __forceinline__ Lds from_pair(int off) const {
+    Lds q = *this;
+    q.P0 += off;
+    q.P1 += off;
+    q.P2 += off;
+    q.P3 += off;
+    q.S0 += off;
+    q.S1 += off;
+    q.W += off;
+    q.P4 += off;
+    return q;
+  }
 };
 
 // LDS: the backward's two partial buffers, or (during the march) lse_mfma's per-wave ray
@@ -1321,8 +1334,10 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
 #endif
   const bool valid = li < a.n_rays;
   long long ri = a.ray_begin + (valid ? li : 0);  // becomes the ray's row in the [N,3] tensors
-  // the wave that writes this ray's outputs and runs its post-march forward and backward
+  // the wave that writes this ray's outputs; SPLIT: all four waves run the post-march forward
+  // (each over a quarter of the spheres, merged) and wave w seeds the backward of lanes 16w..16w+15
   const bool own_rays = !SPLIT || wave == 0;
+  const bool seed_lane = !SPLIT || (lane >> 4) == wave;
 
   const float kappa = a.k * kLog2e, nkappa = -kappa, inv_kappa = 1.0f / kappa;
 
@@ -1373,6 +1388,64 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     else
       for_tiles([&](int, int tn) { lse_point<true, kShiftMax>(p, L, tn / 2, nkappa, m, s); });
     return -(flog2(fmaxf(s, 1e-8f)) + m) * inv_kappa;
+  };
+  // SPLIT: the post-march vector sweeps of a 64-ray block run on its four waves, wave w over the
+  // pairs [split_pair(w), split_pair(w + 1)) (multiples of 8), and the partial states are merged
+  // through LDS in wave order (every wave then holds the same totals).
+  auto split_pair = [&](int w) { return (((a.Mpad / 2) * w) / kSplitWaves) & ~7; };
+  auto soft_min_split = [&](const float p[3], bool fast, float& m, float& s) {
+    const int b0 = split_pair(wave), b1 = split_pair(wave + 1);
+    const Lds Lq = L.from_pair(b0);
+    m = -INFINITY;
+    s = 0.0f;
+    if (fast) lse_point<false, kShiftMax>(p, Lq, b1 - b0, nkappa, m, s);
+    else lse_point<true, kShiftMax>(p, Lq, b1 - b0, nkappa, m, s);
+    float* xm = L.slots;
+    float* xs = L.slots + kSplitWaves * 64;
+    __syncthreads();  // the march's last exchange is read
+    xm[wave * 64 + lane] = m;
+    xs[wave * 64 + lane] = s;
+    __syncthreads();
+    float mm = xm[lane];
+#pragma unroll
+    for (int w = 1; w < kSplitWaves; ++w) mm = fmaxf(mm, xm[w * 64 + lane]);
+    float ss = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kSplitWaves; ++w) ss += xs[w * 64 + lane] * fexp2(xm[w * 64 + lane] - mm);
+    m = mm;
+    s = ss;
+    return -(flog2(fmaxf(s, 1e-8f)) + m) * inv_kappa;
+  };
+  // shade_normal_sweep's state (dmin; colour sums at c10l, mask and normal sums at kappa, each
+  // relative to dmin) merged over the four waves; the totals come back in the .x lanes
+  auto shade_merge = [&](float c10l, float& dmin, f2& Zw, f2 (&C)[3], f2& Zb, f2 (&G)[3]) {
+    constexpr int kF = 9;
+    float* xb = L.slots + 2 * kSplitWaves * 64;  // [kF][wave][64], after soft_min_split's buffers
+    const float v[kF] = {dmin, Zw.x + Zw.y, C[0].x + C[0].y, C[1].x + C[1].y, C[2].x + C[2].y,
+                         Zb.x + Zb.y, G[0].x + G[0].y, G[1].x + G[1].y, G[2].x + G[2].y};
+#pragma unroll
+    for (int f = 0; f < kF; ++f) xb[(f * kSplitWaves + wave) * 64 + lane] = v[f];
+    __syncthreads();
+    float dm = xb[lane];
+#pragma unroll
+    for (int w = 1; w < kSplitWaves; ++w) dm = fminf(dm, xb[w * 64 + lane]);
+    float acc[kF - 1] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int w = 0; w < kSplitWaves; ++w) {
+      const float dw = xb[w * 64 + lane];
+      const float sw = fexp2((dm - dw) * c10l), sb = fexp2((dm - dw) * kappa);
+#pragma unroll
+      for (int f = 1; f < kF; ++f) acc[f - 1] = fmaf(xb[(f * kSplitWaves + w) * 64 + lane], f < 5 ? sw : sb, acc[f - 1]);
+    }
+    dmin = dm;
+    Zw = f2{acc[0], 0.0f};
+    C[0] = f2{acc[1], 0.0f};
+    C[1] = f2{acc[2], 0.0f};
+    C[2] = f2{acc[3], 0.0f};
+    Zb = f2{acc[4], 0.0f};
+    G[0] = f2{acc[5], 0.0f};
+    G[1] = f2{acc[6], 0.0f};
+    G[2] = f2{acc[7], 0.0f};
   };
   // The march's soft-min with the cheapest safe shift (the result differs only by fp32 rounding).
   // kShiftNone needs the hard maximum -kappa d_min >= -100 at the new point: d_min(new) <=
@@ -1645,7 +1718,6 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   __builtin_amdgcn_s_setprio(1);
 #endif
   if ((MODE == kFwd || MODE == kRender) && a.t_out != nullptr && valid && own_rays) a.t_out[ri] = t;
-  if (!own_rays) dead = true;  // SPLIT: waves 1-3 are done after the march (zero contributions)
   // work statistics: per wave here in the forward modes; per block at the hand-off barrier in the
   // backward modes (one pair of atomics per block, not per wave)
   if constexpr (MODE == kFwd || MODE == kRender) {
@@ -1668,7 +1740,10 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   if (!dead) {
     // ---- reconnect: t_final = t + sdf(p_approx) (renderer_diff.rs:30-39); renderer.rs has none
     fast_a = all_safe(lb);
-    if constexpr (MODE != kRender) Da = soft_min(pa, fast_a, mA, sA);
+    if constexpr (MODE != kRender) {
+      if constexpr (SPLIT) Da = soft_min_split(pa, fast_a, mA, sA);
+      else Da = soft_min(pa, fast_a, mA, sA);
+    }
     tf = t + Da;
     p[0] = fmaf(d[0], tf, o[0]);
     p[1] = fmaf(d[1], tf, o[1]);
@@ -1684,8 +1759,16 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     if constexpr (MODE != kRender) {
       // one sweep for both: f = 2 eps grad D (its eps -> 0 limit) with grad D = G / Zb
       f2 G2[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
-      if (fast_f) shade_normal_sweep<false>(p, L, a.Mpad / 2, c10l, kappa, dmin, Zw2, C2, Zb2, G2);
-      else shade_normal_sweep<true>(p, L, a.Mpad / 2, c10l, kappa, dmin, Zw2, C2, Zb2, G2);
+      if constexpr (SPLIT) {  // this wave's quarter of the pairs, then the four partial states merged
+        const int b0 = split_pair(wave), b1 = split_pair(wave + 1);
+        const Lds Lq = L.from_pair(b0);
+        if (fast_f) shade_normal_sweep<false>(p, Lq, b1 - b0, c10l, kappa, dmin, Zw2, C2, Zb2, G2);
+        else shade_normal_sweep<true>(p, Lq, b1 - b0, c10l, kappa, dmin, Zw2, C2, Zb2, G2);
+        shade_merge(c10l, dmin, Zw2, C2, Zb2, G2);
+      } else {
+        if (fast_f) shade_normal_sweep<false>(p, L, a.Mpad / 2, c10l, kappa, dmin, Zw2, C2, Zb2, G2);
+        else shade_normal_sweep<true>(p, L, a.Mpad / 2, c10l, kappa, dmin, Zw2, C2, Zb2, G2);
+      }
       const float te = 2.0f * a.eps * frcp(Zb2.x + Zb2.y);
       const float nx = te * (G2[0].x + G2[0].y), ny = te * (G2[1].x + G2[1].y), nz = te * (G2[2].x + G2[2].y);
       const float inv_len = frsq(fmaf(nz, nz, fmaf(ny, ny, fmaf(nx, nx, 1e-6f))));
@@ -1790,7 +1873,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   // ---- seed g = dL/dout
   float g[3] = {0.0f, 0.0f, 0.0f};
   float loss = 0.0f;
-  if (valid && own_rays) {
+  if (valid && seed_lane) {
     if constexpr (MODE == kBwd) {
       g[0] = a.gout[3 * ri];
       g[1] = a.gout[3 * ri + 1];
