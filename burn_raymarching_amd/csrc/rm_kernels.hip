@@ -80,9 +80,14 @@ enum Mode { kFwd = 0, kBwd = 1, kTrain = 2, kRender = 3 };
 
 // bounds the partial-gradient workspace per launch: 16 views of 512x512
 constexpr int kMaxBlocksPerLaunch = 16384 * (256 / kBlock);
-// automatic split march (RM_MARCH_SPLIT): from this many spheres, for launches of at most this
-// many rays (about one fill of the GPU: 1024 resident 256-ray blocks)
-constexpr int kSplitMinSpheres = 2048;
+// automatic split march (RM_MARCH_SPLIT): from kSplitMinSpheres spheres for launches of at most
+// kSplitMaxRays rays (about one fill of the GPU: 1024 resident 256-ray blocks), from
+// kSplitMinSpheresWide for launches of at most kSplitMaxRaysWide (four fills) -- measured
+// (tools/gpu_split_sweep.sh): split wins at 1 view from 256 spheres and at 4 views of 512x512
+// from 512, loses at 10 views of 256 spheres and at 4 views of 1024x1024
+constexpr int kSplitMinSpheres = 256;
+constexpr int kSplitMinSpheresWide = 512;
+constexpr long long kSplitMaxRaysWide = 1048576;
 #ifndef RM_SPLIT_WAVES
 #define RM_SPLIT_WAVES 4
 #endif
@@ -2926,8 +2931,8 @@ int run(rm_context* ctx, const Call& c) {
   // Escape skipping needs the mask to be exactly 0 at the certified distance: sigmoid(-msharp D)
   // once msharp log2(e) D > 128 overflows exp2 (use 160), exp(-10 D^2) in kRender long before 50.
   const bool mask_vanishes = c.mode == kRender || a.msharp > 0.0f;
-  // Split march (RM_MARCH_SPLIT): forced by the flag or env RM_SPLIT=1, automatic from
-  // kSplitMinSpheres spheres when the launch fills the GPU at most about once; never with
+  // Split march (RM_MARCH_SPLIT): forced by the flag or env RM_SPLIT=1, automatic by sphere count
+  // and rays per launch (kSplitMinSpheres / kSplitMaxRays, kSplitMinSpheresWide / ...Wide); never with
   // RM_MARCH_NO_SPLIT / env RM_SPLIT=0, in the renderer.rs mode or with the escape pre-pass.
   bool split = false;
   if (c.mode != kRender && (c.march->flags & RM_MARCH_SKIP_ESCAPED) == 0) {
@@ -2935,7 +2940,7 @@ int run(rm_context* ctx, const Call& c) {
     const long long n_all = c.cam ? (long long)c.views * c.W * c.H : c.n;
     if ((c.march->flags & RM_MARCH_SPLIT) != 0 || (e && e[0] == '1')) split = true;
     else if ((c.march->flags & RM_MARCH_NO_SPLIT) == 0 && !(e && e[0] == '0'))
-      split = M >= kSplitMinSpheres && n_all <= kSplitMaxRays;
+      split = (M >= kSplitMinSpheres && n_all <= kSplitMaxRays) || (M >= kSplitMinSpheresWide && n_all <= kSplitMaxRaysWide);
   }
   a.split = split ? 1 : 0;
   const int rpb = split ? 64 : kBlock;  // rays per block

@@ -119,12 +119,12 @@ typedef struct rm_march {
 /* Split march: a ray block takes 64 rays (one 8x8 pixel quadrant in camera mode) held by all
  * four waves of the block; every march step each wave sums a quarter of the spheres on the
  * matrix cores and the quarters are added in a fixed order, so the waves march in lockstep;
- * the post-march forward and the backward run on the first wave. A ray that marches every
- * step then spreads over four SIMDs: for many spheres when one launch fills the GPU about once
- * (BASELINE configs[4]), where a few rays march all steps while the rest leave early. Taken
- * automatically from 2048 spheres for launches of at most 262,144 rays; this flag forces it,
- * RM_MARCH_NO_SPLIT forbids it. Results agree to fp32 rounding (the sphere sums are added in
- * another order). */
+ * the post-march sweeps are split the same way and each wave seeds the backward of a quarter of
+ * the rays. A ray that marches every step then spreads over four SIMDs: for launches that fill
+ * the GPU a few times (BASELINE configs[4]), where a few rays march all steps while the rest
+ * leave early. Taken automatically from 256 spheres for launches of at most 262,144 rays and
+ * from 512 spheres for at most 1,048,576 rays; this flag forces it, RM_MARCH_NO_SPLIT forbids
+ * it. Results agree to fp32 rounding (the sphere sums are added in another order). */
 #define RM_MARCH_SPLIT 512
 #define RM_MARCH_NO_SPLIT 1024
 

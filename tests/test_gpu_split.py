@@ -8,7 +8,8 @@ wave summing a quarter of the sphere row blocks per march step, the quarters add
   * bit-for-bit properties the unsplit march has too: early exit on / off, shared origin step /
     per-ray first step, three consecutive train calls (the 2nd and 3rd in the cost order of the
     call before), camera mode in row order / array mode on the same rays, ragged ray counts;
-  * the automatic choice (>= 2048 spheres, <= 262,144 rays per launch) and RM_MARCH_NO_SPLIT.
+  * the automatic choice (>= 256 spheres and <= 262,144 rays per launch, or >= 512 spheres and
+    <= 1,048,576 rays) and RM_MARCH_NO_SPLIT.
 Tolerances as in tests/test_gpu_parity.py.
 """
 import numpy as np
@@ -147,8 +148,8 @@ def test_split_array_mode_and_ragged(rm, oracle, monkeypatch):
 
 
 def test_split_automatic_choice(rm, monkeypatch):
-    """From 2048 spheres the split march is taken automatically for launches of at most 262,144
-    rays (the same bits as RM_SPLIT=1); RM_MARCH_NO_SPLIT gives the unsplit bits."""
+    """2048 spheres on a 32x32 view: the split march is taken automatically (the same bits as
+    RM_SPLIT=1); RM_MARCH_NO_SPLIT gives the unsplit bits."""
     render, model, native = rm
     M, S, K = 2048, 16, 32.0
     s = model.scene_tensors(model.synthetic_scene(M, 16, radius_range=(0.01, 0.04)))
