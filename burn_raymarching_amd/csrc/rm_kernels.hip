@@ -425,6 +425,7 @@ __device__ void write_bound(const KArgs& a, float* hdr, float* esc) {
 // rm_prep_finish); the final header also gets the scene's bounding sphere (scene_bound).
 constexpr int kPrepStageMax = 512;  // one-block prep: parameters staged in LDS up to this M
 
+template <bool PAR>
 __device__ void write_origins(const KArgs& a, const float4& S00, const float4& S10, float rmax, float spread,
                               const uint4* At, const float* Wt, float* orig, unsigned char* xch, int v);
 
@@ -545,15 +546,19 @@ __global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, float* __re
 // The per-view origin steps (write_origins), one 64-thread block (one wave) per view, after the
 // records are complete: the views run on separate CUs side by side.
 // A split launch's origin step runs its four quarters on four waves of the block (the split
-// march's own combine, same order as lse_mfma_quarters: the same bits).
+// march's own combine: the same bits).
 constexpr int kOriginXch = 64 * 36;  // bytes of march exchange per wave
-__global__ __launch_bounds__(256) void rm_origin_kernel(const KArgs a, const float4* __restrict__ rec, int nprep) {
-  __shared__ __attribute__((aligned(16))) unsigned char xch[kSplitWaves * kOriginXch + kSplitWaves * 64 * 4];
+template <bool SPLIT>
+__global__ __launch_bounds__(SPLIT ? 64 * kSplitWaves : 64) void rm_origin_kernel(const KArgs a,
+                                                                                 const float4* __restrict__ rec,
+                                                                                 int nprep) {
+  __shared__ __attribute__((aligned(16))) unsigned char xch[SPLIT ? kSplitWaves * kOriginXch + kSplitWaves * 64 * 4
+                                                                  : kOriginXch];
   const int np = a.Mpad / 2;
   const uint4* At = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(rec) + tiles_offset(np, nprep));
   const float* Wt = reinterpret_cast<const float*>(At + (size_t)(np / 8) * 64);
   const float* hdr = reinterpret_cast<const float*>(reinterpret_cast<const float2*>(rec + 7 * (size_t)np) + np);
-  write_origins(a, rec[4 * np], rec[5 * np], hdr[1], hdr[2], At, Wt, a.origin, xch, blockIdx.x);
+  write_origins<SPLIT>(a, rec[4 * np], rec[5 * np], hdr[1], hdr[2], At, Wt, a.origin, xch, blockIdx.x);
 }
 
 // ---- packed helpers --------------------------------------------------------------------------
@@ -757,39 +762,17 @@ __device__ __forceinline__ float split_combine(float part, float* comb, int wave
   for (int w = 1; w < kSplitWaves; ++w) s += comb[w * 64 + lane];
   return s;
 }
-// The matrix-core sum over all row blocks as a split block forms it: the four quarters' sums
-// added in wave order (one wave computing every quarter: the origin step of a split launch).
-template <bool CLAMP, bool FIXED>
-__device__ __forceinline__ float lse_mfma_quarters(const float p[3], float k2, float sh, const uint4* __restrict__ At,
-                                                   const float* __restrict__ Wt, int nrb, uint4* xa, uint4* xb,
-                                                   float* xs, int lane) {
-  float s = 0.0f;
-#pragma unroll
-  for (int w = 0; w < kSplitWaves; ++w) {
-    const int r0 = part_rb(nrb, w), r1 = part_rb(nrb, w + 1);
-    const float q = lse_mfma<CLAMP, FIXED>(p, k2, sh, At + (size_t)r0 * 64, Wt + (size_t)r0 * 32, r1 - r0, xa, xb, xs,
-                                           lane);
-    s = w == 0 ? q : s + q;
-  }
-  return s;
-}
-
 // A march step's soft-min D at p on the matrix cores without a shift (soft_min_march's
 // unshifted step; shared with write_origins like march_d_fixed). comb != nullptr: a split
-// block's wave, At / Wt / nrb its quarter (split_combine); quarters: all quarters in one wave.
+// block's wave, At / Wt / nrb its quarter (split_combine).
 template <bool CLAMP, bool BUF = (RM_MARCH_BUFLOAD != 0)>
 __device__ __forceinline__ float march_d_none(const float p[3], float kappa, float inv_kappa,
                                               const uint4* __restrict__ At, const float* __restrict__ Wt, int nrb,
                                               uint4* xa, uint4* xb, float* xs, int lane, float* comb = nullptr,
-                                              int wave = 0, bool quarters = false) {
+                                              int wave = 0) {
 #pragma clang fp contract(off)
-  float s;
-  if (quarters) {
-    s = lse_mfma_quarters<CLAMP, false>(p, kappa * kappa, 0.0f, At, Wt, nrb, xa, xb, xs, lane);
-  } else {
-    s = lse_mfma<CLAMP, false, BUF>(p, kappa * kappa, 0.0f, At, Wt, nrb, xa, xb, xs, lane);
-    if (comb != nullptr) s = split_combine(s, comb, wave, lane);
-  }
+  float s = lse_mfma<CLAMP, false, BUF>(p, kappa * kappa, 0.0f, At, Wt, nrb, xa, xb, xs, lane);
+  if (comb != nullptr) s = split_combine(s, comb, wave, lane);
   return -flog2(fmaxf(s, 1e-30f)) * inv_kappa;
 }
 
@@ -808,18 +791,12 @@ template <bool CLAMP, bool BUF = (RM_MARCH_BUFLOAD != 0)>
 __device__ __forceinline__ float march_d_fixed(const float p[3], float kappa, float inv_kappa, float kr_first,
                                                const float4& S00, const float4& S10, const uint4* __restrict__ At,
                                                const float* __restrict__ Wt, int nrb, uint4* xa, uint4* xb,
-                                               float* xs, int lane, float* comb = nullptr, int wave = 0,
-                                               bool quarters = false) {
+                                               float* xs, int lane, float* comb = nullptr, int wave = 0) {
 #pragma clang fp contract(off)
   const float k2 = kappa * kappa;
   const float sh = fixed_shift(p, k2, S00, S10);
-  float s;
-  if (quarters) {
-    s = lse_mfma_quarters<CLAMP, true>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
-  } else {
-    s = lse_mfma<CLAMP, true, BUF>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
-    if (comb != nullptr) s = split_combine(s, comb, wave, lane);
-  }
+  float s = lse_mfma<CLAMP, true, BUF>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
+  if (comb != nullptr) s = split_combine(s, comb, wave, lane);
   const float m = kr_first - sh;
   return -(flog2(fmaxf(s, 1e-30f)) + m) * inv_kappa;
 }
@@ -832,6 +809,7 @@ __device__ __forceinline__ float march_d_fixed(const float p[3], float kappa, fl
 // (vector-only march, or the fixed shift not provably safe): those rays march it themselves.
 // rec / hdr: this call's complete records and header; At / Wt: its march tiles; xch: 64 x 36 B
 // of LDS. One wave computes view v.
+template <bool PAR>
 __device__ void write_origins(const KArgs& a, const float4& S00, const float4& S10, float rmax, float spread,
                               const uint4* At, const float* Wt, float* orig, unsigned char* xch, int v) {
   const int lane = threadIdx.x & 63;
@@ -840,19 +818,18 @@ __device__ void write_origins(const KArgs& a, const float4& S00, const float4& S
   const bool shift_fixed_ok = kappa * (rmax + spread) * 1.001f <= 100.0f;
   const bool shift_none_ok = kappa * rmax * 1.001f <= 30.0f;
   const float kr_first = kappa * a.radius[0];
-  // a split launch with a block of kSplitWaves waves: wave w sums quarter w, combined in wave
-  // order (split_combine); one wave alone sums the quarters in turn (lse_mfma_quarters)
-  const bool par = a.split != 0 && (int)blockDim.x == 64 * kSplitWaves;
-  const int wave = par ? (int)(threadIdx.x >> 6) : 0;
+  // PAR (a split launch, a block of kSplitWaves waves): wave w sums quarter w, combined in wave
+  // order (split_combine) -- the split march's own sum; else one wave sums every row block
+  const int wave = PAR ? (int)(threadIdx.x >> 6) : 0;
   uint4* xa = reinterpret_cast<uint4*>(xch + wave * kOriginXch);
   uint4* xb = xa + 64;
   float* xs = reinterpret_cast<float*>(xa) + 64 * 8;
-  float* comb = par ? reinterpret_cast<float*>(xch + kSplitWaves * kOriginXch) : nullptr;
+  float* comb = PAR ? reinterpret_cast<float*>(xch + kSplitWaves * kOriginXch) : nullptr;
   const int nrb = np / 8;
   const uint4* Aq = At;
   const float* Wq = Wt;
   int nq = nrb;
-  if (par) {
+  if constexpr (PAR) {
     const int r0 = part_rb(nrb, wave);
     nq = part_rb(nrb, wave + 1) - r0;
     Aq += (size_t)r0 * 64;
@@ -866,10 +843,9 @@ __device__ void write_origins(const KArgs& a, const float4& S00, const float4& S
     const bool none = a.mfma && shift_none_ok && fixed_shift(p, kappa * kappa, S00, S10) - kr_first <= 90.0f;
     // (a split launch's first step adds the four quarters' sums: the same here)
     if (none)
-      D = march_d_none<true>(p, kappa, inv_kappa, Aq, Wq, nq, xa, xb, xs, lane, comb, wave, a.split != 0 && !par);
+      D = march_d_none<true>(p, kappa, inv_kappa, Aq, Wq, nq, xa, xb, xs, lane, comb, wave);
     else if (a.mfma && shift_fixed_ok && psq(p) <= 1e10f)
-      D = march_d_fixed<true>(p, kappa, inv_kappa, kr_first, S00, S10, Aq, Wq, nq, xa, xb, xs, lane, comb, wave,
-                              a.split != 0 && !par);
+      D = march_d_fixed<true>(p, kappa, inv_kappa, kr_first, S00, S10, Aq, Wq, nq, xa, xb, xs, lane, comb, wave);
     if (lane == 0 && wave == 0) orig[v] = D;
   }
 }
@@ -2994,8 +2970,12 @@ int run(rm_context* ctx, const Call& c) {
       RM_HIP(ctx, hipGetLastError());
     }
     if (a.origin != nullptr) {
-      hipLaunchKernelGGL(rm_origin_kernel, dim3(c.views), dim3(a.split ? 64 * kSplitWaves : 64), 0, ctx->stream, a,
-                         (const float4*)ctx->rec, nprep);
+      if (a.split)
+        hipLaunchKernelGGL(rm_origin_kernel<true>, dim3(c.views), dim3(64 * kSplitWaves), 0, ctx->stream, a,
+                           (const float4*)ctx->rec, nprep);
+      else
+        hipLaunchKernelGGL(rm_origin_kernel<false>, dim3(c.views), dim3(64), 0, ctx->stream, a, (const float4*)ctx->rec,
+                           nprep);
       RM_HIP(ctx, hipGetLastError());
     }
     a.rec_buf = (const float4*)ctx->rec;
