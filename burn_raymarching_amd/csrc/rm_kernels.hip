@@ -1457,7 +1457,11 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       tr_paths += 1ull << (16 * ((fixed ? 2 : 0) + (fast ? 0 : 1)));
 #endif
       float Dm;
-      constexpr bool kBuf = RM_MARCH_BUFLOAD != 0 && !SPLIT;  // split: global loads (measured faster)
+#ifndef RM_SPLIT_BUFLOAD
+#define RM_SPLIT_BUFLOAD 0
+#endif
+      // split: global loads (measured faster)
+      constexpr bool kBuf = RM_MARCH_BUFLOAD != 0 && (!SPLIT || RM_SPLIT_BUFLOAD != 0);
       const uint4* At = L.At;
       const float* Wt = L.Wt;
       int nq = nrb;
