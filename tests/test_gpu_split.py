@@ -165,3 +165,21 @@ def test_split_automatic_choice(rm, monkeypatch):
     _equal(auto, forced)
     _equal(no, off)
     assert not np.array_equal(auto[2], off[2])
+
+
+@pytest.mark.parametrize("m,views,size,split", [(256, 1, 64, True), (512, 4, 96, True), (256, 10, 512, False),
+                                                (128, 1, 64, False)])
+def test_split_threshold(rm, monkeypatch, m, views, size, split):
+    """The automatic choice at the thresholds: 256 spheres split up to 262,144 rays per launch,
+    512 spheres up to 1,048,576; 10 views of 512x512 at 256 spheres (the bench metric) and fewer
+    than 256 spheres stay unsplit. The automatic run equals (==) the forced one it picks."""
+    render, model, native = rm
+    S, K = 16, 32.0
+    s = model.scene_tensors(model.synthetic_scene(m, 21, radius_range=(0.02, 0.08)))
+    cams = model.ring_cameras(10)[:views]
+    tg = render.render_diff_camera(cams, size, size, model.scene_tensors(model.synthetic_scene(m, 22)), K, S)
+    monkeypatch.delenv("RM_SPLIT", raising=False)
+    auto = _train(render, native, cams, size, size, tg, s, K, S)
+    forced = _train(render, native, cams, size, size, tg, s, K, S,
+                    flags=native.RM_MARCH_SPLIT if split else native.RM_MARCH_NO_SPLIT)
+    _equal(auto, forced)
