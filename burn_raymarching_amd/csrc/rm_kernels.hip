@@ -155,6 +155,16 @@ struct KArgs {
   float* dbg;       // optional per-ray intermediates [n][16] (diagnostics; see rm_debug_intermediates)
   float* partials;  // [gridDim.x][rec], rec = Mpad*8 + 8
   long long rec;
+  // Continuation of a split launch (split_cont_steps, see run()): with cont_cap > 0 a block whose
+  // rays still march at step cont_cap saves its march state and its logical block and ends; a
+  // second launch with cont_resume = that step runs the saved blocks (cont_list[0..*cont_count))
+  // from there. cont_state: [6][cont_rays] per ray (t, lb, D_prev, t one and two steps back,
+  // gone) then [blocks][2] per block (choice history, steps saved).
+  int cont_cap, cont_resume;
+  float* cont_state;
+  int* cont_list;
+  int* cont_count;
+  long long cont_rays;
 #ifdef RM_BLOCK_TRACE
   unsigned long long* btrace;  // measurement build: per-wave timing records (rm_ray_kernel)
 #endif
@@ -1306,7 +1316,13 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int cls = -1;  // the block's cost class in the previous launch (cost-ordered dispatch), else -1
-  const long long blk = ray_block(a, &cls);
+  long long blk;
+  if (SPLIT && a.cont_resume > 0) {  // continuation launch: the blocks the first launch deferred
+    if ((int)blockIdx.x >= *a.cont_count) return;
+    blk = a.cont_list[blockIdx.x];
+  } else {
+    blk = ray_block(a, &cls);
+  }
   const long long li = SPLIT ? blk * 64 + lane : blk * kBlock + tid;
 #if RM_HEAVY_PRIO
   // the dearest class's waves first at the SIMD's issue arbiter: they set the launch's critical
@@ -1588,7 +1604,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       // Camera mode: step 0 from the soft-min at the eye, evaluated once per view by the same
       // code path (write_origins), when every lane of the wave has it (not NaN). Taken before
       // the loop so that D0 holds no register through the march.
-      if (a.origin != nullptr && a.steps > 0) {
+      if (a.origin != nullptr && a.steps > 0 && !(SPLIT && a.cont_resume > 0)) {
         const float D0 = a.origin[view];
         if (__all((__float_as_uint(D0) & 0x7fffffffu) <= 0x7f800000u)) {
           const float p[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
@@ -1614,7 +1630,39 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     float cyc_t4 = __builtin_nanf("");
 #endif
     int chist = 0xFFF;
+    static_assert(RM_CYCLE_MAX == 2 || !SPLIT, "the continuation saves two steps of history");
+    if (SPLIT && a.cont_resume > 0) {  // the state the first launch saved at step cont_resume
+      const float* cs = a.cont_state;
+      const long long R = a.cont_rays;
+      t = cs[li];
+      lb = cs[R + li];
+      Dprev = cs[2 * R + li];
+      cyc_t1 = cs[3 * R + li];
+      cyc_t2 = cs[4 * R + li];
+      gone = cs[5 * R + li] != 0.0f;
+      chist = __float_as_int(cs[6 * R + 2 * blk]);
+      steps_saved = __float_as_int(cs[6 * R + 2 * blk + 1]);
+      st0 = a.cont_resume;
+    }
     for (int st = st0; !dead && st < a.steps; ++st) {
+      if (SPLIT && a.cont_cap > 0 && st == a.cont_cap) {  // defer: save the state at the top of this step
+        if (wave == 0) {  // the four waves hold the same state
+          float* cs = a.cont_state;
+          const long long R = a.cont_rays;
+          cs[li] = t;
+          cs[R + li] = lb;
+          cs[2 * R + li] = Dprev;
+          cs[3 * R + li] = cyc_t1;
+          cs[4 * R + li] = cyc_t2;
+          cs[5 * R + li] = gone ? 1.0f : 0.0f;
+          if (lane == 0) {
+            cs[6 * R + 2 * blk] = __int_as_float(chist);
+            cs[6 * R + 2 * blk + 1] = __int_as_float(steps_saved);
+            a.cont_list[atomicAdd(a.cont_count, 1)] = (int)blk;
+          }
+        }
+        return;
+      }
 #if RM_PRIO_RAMP
       if (st == half) __builtin_amdgcn_s_setprio(2);
 #endif
@@ -2639,6 +2687,8 @@ struct rm_context {
   int order_tx = 0, order_ty = 0, order_sub = 0;
   int* olist = nullptr;                     // cost-ordered dispatch: 3 x [class][kMaxBlocksPerLaunch] block lists
   int* ocnt = nullptr;                      // 3 x [class] list lengths (zeroed one launch ahead)
+  float* cont_buf = nullptr;                // split continuation: saved march state | list | count
+  size_t cont_bytes = 0;
   int oturn = 0;                            // the list set the next keyed launch appends to
   unsigned long long cost_key = 0;          // geometry of the last keyed launch (its lists order the next)
   bool cost_valid = false;
@@ -2722,6 +2772,15 @@ long long max_blocks_per_launch() {
 }
 
 long long rec_floats(int Mpad) { return (long long)Mpad * 8 + 8; }
+
+// March steps after which a split launch hands the blocks still marching to a continuation
+// launch: env RM_SPLIT_CONT_STEPS (0 = one launch), else max(32, 3 S / 8) for S >= 64 march steps
+// (measured, tools/gpu_env_ab.sh: at 4096 spheres S = 128 step 48 gave -20 %, S = 64 step 32 -8 %;
+// at S = 32 any step was slower).
+int split_cont_steps(int steps) {
+  if (const char* e = std::getenv("RM_SPLIT_CONT_STEPS")) return std::max(0, std::atoi(e));
+  return steps >= 64 ? std::max(32, 3 * steps / 8) : 0;
+}
 
 size_t ws_need(long long max_rays, int M, int rays_per_block = kBlock) {
   const int Mpad = pad_spheres(M);
@@ -3089,11 +3148,60 @@ int run(rm_context* ctx, const Call& c) {
       a.btrace = ctx->btrace;
       ctx->btrace_waves = nb * kWaves;
 #endif
+      // Split continuation (bwd / train launches with the early exit): the blocks still marching
+      // at step cont_steps stop there, and a second launch runs just those from their saved
+      // state, dispatched one after another at its front -- spread evenly over the CUs, where the
+      // first launch placed them by a cost order that only partly predicts which 64-ray groups
+      // march every step. Bit-identical to one launch (tests/test_gpu_split.py).
+      const int cont_steps = split_cont_steps(a.steps);
+      const bool cont = split && c.mode != kRender && c.mode != kFwd && a.early_exit && cont_steps > 0 &&
+                        a.steps >= 2 * cont_steps;
+      if (cont) {
+        const long long rays = nb * 64;
+        const size_t need = (size_t)(6 * rays + 2 * nb) * sizeof(float) + (size_t)(nb + 16) * sizeof(int);
+        if (ctx->cont_bytes < need) {
+          if (ctx->cont_buf) RM_HIP(ctx, hipFree(ctx->cont_buf));
+          ctx->cont_buf = nullptr;
+          ctx->cont_bytes = 0;
+          RM_HIP(ctx, hipMalloc(&ctx->cont_buf, need));
+          ctx->cont_bytes = need;
+        }
+        a.cont_state = ctx->cont_buf;
+        a.cont_rays = rays;
+        a.cont_list = reinterpret_cast<int*>(ctx->cont_buf + 6 * rays + 2 * nb);
+        a.cont_count = a.cont_list + nb;
+        a.cont_cap = cont_steps;
+        a.cont_resume = 0;
+        RM_HIP(ctx, hipMemsetAsync(a.cont_count, 0, sizeof(int), ctx->stream));
+      }
       if (c.mode == kFwd) launch_ray<kFwd>(c.cam, split, grid, lds, ctx->stream, a, ev0, ev1);
       else if (c.mode == kBwd) launch_ray<kBwd>(c.cam, split, grid, lds, ctx->stream, a, ev0, ev1);
       else if (c.mode == kTrain) launch_ray<kTrain>(c.cam, split, grid, lds, ctx->stream, a, ev0, ev1);
       else launch_ray<kRender>(c.cam, false, grid, lds, ctx->stream, a, ev0, ev1);
       RM_HIP(ctx, hipGetLastError());
+      if (cont) {
+        KArgs b = a;
+        b.cont_cap = 0;
+        b.cont_resume = cont_steps;
+        b.ocnt_z = nullptr;  // cleared by the first launch
+        b.olist_r = nullptr;
+        b.ocnt_r = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (ctx->timing) {
+          if (ctx->events_used == ctx->events.size()) {
+            std::pair<hipEvent_t, hipEvent_t> pr;
+            RM_HIP(ctx, hipEventCreate(&pr.first));
+            RM_HIP(ctx, hipEventCreate(&pr.second));
+            ctx->events.push_back(pr);
+          }
+          e0 = ctx->events[ctx->events_used].first;
+          e1 = ctx->events[ctx->events_used].second;
+          ++ctx->events_used;
+        }
+        if (c.mode == kBwd) launch_ray<kBwd>(c.cam, true, grid, lds, ctx->stream, b, e0, e1);
+        else launch_ray<kTrain>(c.cam, true, grid, lds, ctx->stream, b, e0, e1);
+        RM_HIP(ctx, hipGetLastError());
+      }
     }
     if (has_bwd) {
       const int nblocks = (int)nb;
@@ -3246,12 +3354,13 @@ int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset) {
 
 void rm_destroy(rm_context* ctx) {
   if (!ctx) return;
-  if (ctx->stats_dev || ctx->esc_flags || ctx->rec || ctx->block_order || ctx->olist) {
+  if (ctx->stats_dev || ctx->esc_flags || ctx->rec || ctx->block_order || ctx->olist || ctx->cont_buf) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stats_dev) (void)hipFree(ctx->stats_dev);
     if (ctx->esc_flags) (void)hipFree(ctx->esc_flags);
     if (ctx->block_order) (void)hipFree(ctx->block_order);
     if (ctx->olist) (void)hipFree(ctx->olist);
+    if (ctx->cont_buf) (void)hipFree(ctx->cont_buf);
     if (ctx->ocnt) (void)hipFree(ctx->ocnt);
     if (ctx->rec) (void)hipFree(ctx->rec);
   }

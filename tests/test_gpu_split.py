@@ -183,3 +183,34 @@ def test_split_threshold(rm, monkeypatch, m, views, size, split):
     forced = _train(render, native, cams, size, size, tg, s, K, S,
                     flags=native.RM_MARCH_SPLIT if split else native.RM_MARCH_NO_SPLIT)
     _equal(auto, forced)
+
+
+def test_split_continuation(rm, oracle, monkeypatch):
+    """Continuation launch (split train / backward launches with S >= 64: the blocks still marching
+    at step max(32, 3S/8) stop, and a second launch runs them from their saved march state):
+    bit-identical to one launch (RM_SPLIT_CONT_STEPS=0), to other continuation steps and to the
+    march with the early exit off; the timed launches show the second launch; the image is within
+    the oracle's tolerance."""
+    render, model, native = rm
+    W = H = 64
+    M, S, K = 300, 64, 32.0
+    sc = model.synthetic_scene(M, 23, radius_range=(0.02, 0.08))
+    s = model.scene_tensors(sc)
+    cams = model.ring_cameras(10, offset=3)[:2]
+    tg = render.render_diff_camera(cams, W, H, model.scene_tensors(model.synthetic_scene(M, 24)), K, S)
+    monkeypatch.setenv("RM_SPLIT", "1")
+    monkeypatch.delenv("RM_SPLIT_CONT_STEPS", raising=False)
+    ctx = render.context()
+    ctx.collect_timing(reset=True)
+    ctx.timing(True)
+    base = _train(render, native, cams, W, H, tg, s, K, S)
+    ctx.timing(False)
+    _, launches = ctx.collect_timing(reset=True)
+    assert launches == 2
+    for steps in ("0", "8", "31", "40"):
+        monkeypatch.setenv("RM_SPLIT_CONT_STEPS", steps)
+        _equal(base, _train(render, native, cams, W, H, tg, s, K, S))
+    monkeypatch.delenv("RM_SPLIT_CONT_STEPS")
+    _equal(base, _train(render, native, cams, W, H, tg, s, K, S, flags=native.RM_MARCH_NO_EARLY_EXIT))
+    o, d = cam_rays(oracle, cams, W, H)
+    check_fwd(base[2].reshape(-1, 3), oracle.render_diff(o.astype(np.float64), d.astype(np.float64), sc, S, K))
