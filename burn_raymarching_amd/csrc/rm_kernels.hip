@@ -156,14 +156,17 @@ struct KArgs {
   float* partials;  // [gridDim.x][rec], rec = Mpad*8 + 8
   long long rec;
   // Continuation of a split launch (split_cont_steps, see run()): with cont_cap > 0 a block whose
-  // rays still march at step cont_cap saves its march state and its logical block and ends; a
-  // second launch with cont_resume = that step runs the saved blocks (cont_list[0..*cont_count))
-  // from there. cont_state: [6][cont_rays] per ray (t, lb, D_prev, t one and two steps back,
-  // gone) then [blocks][2] per block (choice history, steps saved).
+  // rays still march at step cont_cap saves its march state, appends its logical block to
+  // cont_list_w and ends; a launch with cont_resume = that step runs the saved blocks
+  // (cont_list[0..*cont_count)) from there (and may defer again at its own cont_cap).
+  // cont_state: [6][cont_rays] per ray (t, lb, D_prev, t one and two steps back, gone) then
+  // [blocks][2] per block (choice history, steps saved).
   int cont_cap, cont_resume;
   float* cont_state;
-  int* cont_list;
-  int* cont_count;
+  const int* cont_list;
+  const int* cont_count;
+  int* cont_list_w;
+  int* cont_count_w;
   long long cont_rays;
 #ifdef RM_BLOCK_TRACE
   unsigned long long* btrace;  // measurement build: per-wave timing records (rm_ray_kernel)
@@ -1658,7 +1661,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
           if (lane == 0) {
             cs[6 * R + 2 * blk] = __int_as_float(chist);
             cs[6 * R + 2 * blk + 1] = __int_as_float(steps_saved);
-            a.cont_list[atomicAdd(a.cont_count, 1)] = (int)blk;
+            a.cont_list_w[atomicAdd(a.cont_count_w, 1)] = (int)blk;
           }
         }
         return;
@@ -3153,12 +3156,17 @@ int run(rm_context* ctx, const Call& c) {
       // state, dispatched one after another at its front -- spread evenly over the CUs, where the
       // first launch placed them by a cost order that only partly predicts which 64-ray groups
       // march every step. Bit-identical to one launch (tests/test_gpu_split.py).
-      const int cont_steps = split_cont_steps(a.steps);
-      const bool cont = split && c.mode != kRender && c.mode != kFwd && a.early_exit && cont_steps > 0 &&
-                        a.steps >= 2 * cont_steps;
+      // up to two continuations: at split_cont_steps(S) and (env RM_SPLIT_CONT2_STEPS) later
+      int caps[2] = {split_cont_steps(a.steps), 0};
+      if (const char* e = std::getenv("RM_SPLIT_CONT2_STEPS")) caps[1] = std::max(0, std::atoi(e));
+      const bool cont = split && c.mode != kRender && c.mode != kFwd && a.early_exit && caps[0] > 0 &&
+                        a.steps >= 2 * caps[0];
+      if (!(caps[1] > caps[0] && caps[1] < a.steps)) caps[1] = 0;
+      int* lists[2] = {nullptr, nullptr};
+      int* counts[2] = {nullptr, nullptr};
       if (cont) {
         const long long rays = nb * 64;
-        const size_t need = (size_t)(6 * rays + 2 * nb) * sizeof(float) + (size_t)(nb + 16) * sizeof(int);
+        const size_t need = (size_t)(6 * rays + 2 * nb) * sizeof(float) + (size_t)(2 * nb + 16) * sizeof(int);
         if (ctx->cont_bytes < need) {
           if (ctx->cont_buf) RM_HIP(ctx, hipFree(ctx->cont_buf));
           ctx->cont_buf = nullptr;
@@ -3166,23 +3174,31 @@ int run(rm_context* ctx, const Call& c) {
           RM_HIP(ctx, hipMalloc(&ctx->cont_buf, need));
           ctx->cont_bytes = need;
         }
+        lists[0] = reinterpret_cast<int*>(ctx->cont_buf + 6 * rays + 2 * nb);
+        lists[1] = lists[0] + nb;
+        counts[0] = lists[1] + nb;
+        counts[1] = counts[0] + 1;
         a.cont_state = ctx->cont_buf;
         a.cont_rays = rays;
-        a.cont_list = reinterpret_cast<int*>(ctx->cont_buf + 6 * rays + 2 * nb);
-        a.cont_count = a.cont_list + nb;
-        a.cont_cap = cont_steps;
+        a.cont_list_w = lists[0];
+        a.cont_count_w = counts[0];
+        a.cont_cap = caps[0];
         a.cont_resume = 0;
-        RM_HIP(ctx, hipMemsetAsync(a.cont_count, 0, sizeof(int), ctx->stream));
+        RM_HIP(ctx, hipMemsetAsync(counts[0], 0, 2 * sizeof(int), ctx->stream));
       }
       if (c.mode == kFwd) launch_ray<kFwd>(c.cam, split, grid, lds, ctx->stream, a, ev0, ev1);
       else if (c.mode == kBwd) launch_ray<kBwd>(c.cam, split, grid, lds, ctx->stream, a, ev0, ev1);
       else if (c.mode == kTrain) launch_ray<kTrain>(c.cam, split, grid, lds, ctx->stream, a, ev0, ev1);
       else launch_ray<kRender>(c.cam, false, grid, lds, ctx->stream, a, ev0, ev1);
       RM_HIP(ctx, hipGetLastError());
-      if (cont) {
+      for (int ph = 0; cont && ph < 2 && caps[ph] > 0; ++ph) {
         KArgs b = a;
-        b.cont_cap = 0;
-        b.cont_resume = cont_steps;
+        b.cont_resume = caps[ph];
+        b.cont_list = lists[ph];
+        b.cont_count = counts[ph];
+        b.cont_cap = ph == 0 ? caps[1] : 0;  // the second continuation, if any
+        b.cont_list_w = lists[1];
+        b.cont_count_w = counts[1];
         b.ocnt_z = nullptr;  // cleared by the first launch
         b.olist_r = nullptr;
         b.ocnt_r = nullptr;

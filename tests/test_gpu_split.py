@@ -200,6 +200,7 @@ def test_split_continuation(rm, oracle, monkeypatch):
     tg = render.render_diff_camera(cams, W, H, model.scene_tensors(model.synthetic_scene(M, 24)), K, S)
     monkeypatch.setenv("RM_SPLIT", "1")
     monkeypatch.delenv("RM_SPLIT_CONT_STEPS", raising=False)
+    monkeypatch.delenv("RM_SPLIT_CONT2_STEPS", raising=False)
     ctx = render.context()
     ctx.collect_timing(reset=True)
     ctx.timing(True)
@@ -211,6 +212,14 @@ def test_split_continuation(rm, oracle, monkeypatch):
         monkeypatch.setenv("RM_SPLIT_CONT_STEPS", steps)
         _equal(base, _train(render, native, cams, W, H, tg, s, K, S))
     monkeypatch.delenv("RM_SPLIT_CONT_STEPS")
+    # a second continuation (three launches)
+    monkeypatch.setenv("RM_SPLIT_CONT2_STEPS", "48")
+    ctx.collect_timing(reset=True)
+    ctx.timing(True)
+    _equal(base, _train(render, native, cams, W, H, tg, s, K, S))
+    ctx.timing(False)
+    assert ctx.collect_timing(reset=True)[1] == 3
+    monkeypatch.delenv("RM_SPLIT_CONT2_STEPS")
     _equal(base, _train(render, native, cams, W, H, tg, s, K, S, flags=native.RM_MARCH_NO_EARLY_EXIT))
     o, d = cam_rays(oracle, cams, W, H)
     check_fwd(base[2].reshape(-1, 3), oracle.render_diff(o.astype(np.float64), d.astype(np.float64), sc, S, K))
