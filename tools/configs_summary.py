@@ -36,17 +36,22 @@ def main():
                 kern[row["Name"][:90]] = {"calls": int(row["Calls"]), "avg_us": round(float(row["AverageNs"]) / 1e3, 2)}
             entry["rocprof_kernels"] = kern
             train = next((v for k, v in kern.items() if "rm_ray_kernel<2, true" in k), None)
+            opt = next((v for k, v in kern.items() if "rm_optimizer" in k), None)
             if train:
+                # steps = optimizer calls (one per step); a split launch with a continuation runs the
+                # train kernel twice per step
+                steps = opt["calls"] if opt else train["calls"]
                 entry["rocprof_train_avg_us"] = train["avg_us"]
-                steps = train["calls"]
+                entry["rocprof_train_launches_per_step"] = round(train["calls"] / steps, 2)
+                entry["rocprof_train_us_per_step"] = round(train["avg_us"] * train["calls"] / steps, 2)
                 other = sum(v["avg_us"] * v["calls"] for k, v in kern.items()
                             if k.startswith("rm::") or "rm_optimizer" in k or "rm_ray_kernel<2" in k)
-                entry["rocprof_other_us_per_step"] = round((other - train["avg_us"] * steps) / steps, 2)
+                entry["rocprof_other_us_per_step"] = round((other - train["avg_us"] * train["calls"]) / steps, 2)
         res[name] = entry
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res.items():
         print(k, v["value"], v["ms_per_step"], v.get("train_kernel_ms"), v.get("frac"), v.get("canonical_frac"),
-              v.get("rocprof_train_avg_us"), v.get("rocprof_other_us_per_step"))
+              v.get("rocprof_train_us_per_step"), v.get("rocprof_other_us_per_step"))
 
 
 if __name__ == "__main__":
