@@ -7,6 +7,10 @@ end (s_memrealtime, 100 MHz), hardware slot (XCC, SE, SH, CU, SIMD) and logical 
 position. Prints how busy the SIMDs are over the launch (live waves per SIMD over time, SIMDs with
 at least one live wave), the tail, and how the dispatcher placed consecutive launch positions.
 
+A split launch with a continuation (S >= 64) runs the train kernel twice per step; the records
+then hold the second launch (every block writes one; the ones with nothing to continue end at
+once), unless RM_SPLIT_CONT_STEPS=0.
+
     bash tools/build_variant.sh HEAD trace -DRM_BLOCK_TRACE
     RM_LIB_PATH=burn_raymarching_amd/lib/var/trace.so python tools/block_trace.py --spheres 4096 \
         --march-steps 128 --views 1 --out gpurun_out/trace_c5.npz
