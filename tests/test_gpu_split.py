@@ -223,3 +223,12 @@ def test_split_continuation(rm, oracle, monkeypatch):
     _equal(base, _train(render, native, cams, W, H, tg, s, K, S, flags=native.RM_MARCH_NO_EARLY_EXIT))
     o, d = cam_rays(oracle, cams, W, H)
     check_fwd(base[2].reshape(-1, 3), oracle.render_diff(o.astype(np.float64), d.astype(np.float64), sc, S, K))
+    # the backward mode continues the same way (ragged: 3 views of 40x24 = 45 blocks of 64 rays)
+    import torch
+    cams3 = model.ring_cameras(10, offset=5)[:3]
+    g = torch.randn((3 * 40 * 24, 3), device="cuda", generator=torch.Generator("cuda").manual_seed(7))
+    b0 = {k: host(v) for k, v in render.render_diff_backward_camera(cams3, 40, 24, s, K, g, S).items()}
+    monkeypatch.setenv("RM_SPLIT_CONT_STEPS", "0")
+    b1 = {k: host(v) for k, v in render.render_diff_backward_camera(cams3, 40, 24, s, K, g, S).items()}
+    for key in KEYS:
+        assert np.array_equal(b0[key], b1[key]), key
