@@ -702,7 +702,7 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
   }
   // BUF: buffer loads -- the row block's byte offset in a scalar register, the lane's offset
   // fixed in a vector register, no per-load 64-bit address arithmetic on the vector units (the
-  // unsplit march: +3 %); else global loads (the split march, where buffer loads measured slower)
+  // unsplit march +3 %, the split march +2 % once its quarter bounds are scalar); else global loads
   const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)At, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rw =
       __builtin_amdgcn_make_buffer_rsrc((void*)(Wt + (FIXED ? 16 : 0)), (short)0, 0x7fffffff, 0x00020000);
@@ -833,7 +833,7 @@ __device__ void write_origins(const KArgs& a, const float4& S00, const float4& S
   const float kr_first = kappa * a.radius[0];
   // PAR (a split launch, a block of kSplitWaves waves): wave w sums quarter w, combined in wave
   // order (split_combine) -- the split march's own sum; else one wave sums every row block
-  const int wave = PAR ? (int)(threadIdx.x >> 6) : 0;
+  const int wave = PAR ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;
   uint4* xa = reinterpret_cast<uint4*>(xch + wave * kOriginXch);
   uint4* xb = xa + 64;
   float* xs = reinterpret_cast<float*>(xa) + 64 * 8;
@@ -1317,7 +1317,10 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   L.slots = reinterpret_cast<float*>(smem);
   L.misc = L.slots + kSlotBytes / sizeof(float);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // wave: the wave's index, made scalar (readfirstlane) so that everything derived from it -- a
+  // split wave's quarter of the row blocks, its loop bounds and fragment addresses, LDS slots --
+  // stays wave-uniform for the compiler (threadIdx-derived values are otherwise vector values)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   int cls = -1;  // the block's cost class in the previous launch (cost-ordered dispatch), else -1
   long long blk;
   if (SPLIT && a.cont_resume > 0) {  // continuation launch: the blocks the first launch deferred
@@ -1476,11 +1479,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       tr_paths += 1ull << (16 * ((fixed ? 2 : 0) + (fast ? 0 : 1)));
 #endif
       float Dm;
-#ifndef RM_SPLIT_BUFLOAD
-#define RM_SPLIT_BUFLOAD 0
-#endif
-      // split: global loads (measured faster)
-      constexpr bool kBuf = RM_MARCH_BUFLOAD != 0 && (!SPLIT || RM_SPLIT_BUFLOAD != 0);
+      constexpr bool kBuf = RM_MARCH_BUFLOAD != 0;
       const uint4* At = L.At;
       const float* Wt = L.Wt;
       int nq = nrb;
