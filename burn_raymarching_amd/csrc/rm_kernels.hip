@@ -1981,6 +1981,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   int alive = 0;
 #pragma unroll
   for (int w = 0; w < (SPLIT ? kSplitWaves : kWaves); ++w) alive |= wflag[w] ? 0 : (1 << w);
+  alive = __builtin_amdgcn_readfirstlane(alive);  // block-uniform: scalar for the compiler
   if (dead) {
     if (alive == 0 && wave == 0) {  // the whole block escaped: scalar totals, live flag 0 (the
       if (lane < 8) {               // reduction skips the per-sphere columns, all zero)

@@ -12,6 +12,8 @@ run() {  # name args...
 run m256_s32_v10 --steps 10 && \
 run m256_s64_v10 --march-steps 64 --steps 10 && \
 run m256_s32_v1 --views-per-gpu 1 --steps 10 && \
+run m256_s32_v4 --views-per-gpu 4 --steps 10 && \
+run m256_s64_v4 --march-steps 64 --views-per-gpu 4 --steps 10 && \
 run m256_s128_v1 --march-steps 128 --views-per-gpu 1 --steps 10 && \
 run m512_s32_v1 --spheres 512 --views-per-gpu 1 --steps 10 && \
 run m512_s64_v4 --spheres 512 --march-steps 64 --views-per-gpu 4 --steps 6 && \
