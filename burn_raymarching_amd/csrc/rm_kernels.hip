@@ -3088,12 +3088,8 @@ int run(rm_context* ctx, const Call& c) {
     // cost-ordered dispatch from the previous launch over the same views (single-launch calls)
     const bool has_rec = c.mode == kBwd || c.mode == kTrain;
     unsigned long long key = 0;
-    static const bool env_static = [] {  // RM_STATIC_ORDER=1: as RM_MARCH_STATIC_ORDER (A/B runs)
-      const char* e = std::getenv("RM_STATIC_ORDER");
-      return e != nullptr && e[0] == '1';
-    }();
     if (a.block_order != nullptr && has_rec && nb == blocks_left && done == 0 &&
-        (c.march->flags & RM_MARCH_STATIC_ORDER) == 0 && !env_static) {
+        (c.march->flags & RM_MARCH_STATIC_ORDER) == 0) {
       key = ((unsigned long long)c.W << 48) ^ ((unsigned long long)c.H << 32) ^ ((unsigned long long)c.views << 24) ^
             ((unsigned long long)Mpad << 1) ^ 1ull ^ ((unsigned long long)split << 2);
       constexpr int kCls = RM_ORDER_CLASSES;
