@@ -2366,7 +2366,10 @@ struct FinalArgs {
   int accumulate;
 };
 
-constexpr int kReduceBatch = 8;
+#ifndef RM_REDUCE_BATCH
+#define RM_REDUCE_BATCH 8
+#endif
+constexpr int kReduceBatch = RM_REDUCE_BATCH;  // partial rows in flight per thread
 
 __global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restrict__ P, long long rec, int M, int Mpad,
                                                           int nblocks, int seg_len, float* __restrict__ S) {
