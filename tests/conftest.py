@@ -57,6 +57,32 @@ DANGO = {
 }
 
 
+# Parity margins: every GPU-vs-oracle comparison records its measured error next to its bound,
+# and the session writes them to gpurun_out/parity_margins.json (copied into profiles/ per
+# round), so the committed evidence states how close each case sits to its tolerance.
+_MARGINS = []
+
+
+def record_margin(quantity, err, bound):
+    test = os.environ.get("PYTEST_CURRENT_TEST", "?").split(" ")[0]
+    _MARGINS.append({"test": test, "quantity": quantity, "err": float(err), "bound": float(bound),
+                     "ratio": float(err) / float(bound) if bound > 0 else None})
+
+
+def pytest_sessionfinish(session, exitstatus):
+    if not _MARGINS:
+        return
+    out = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(out, exist_ok=True)
+    worst = {}
+    for m in _MARGINS:
+        q = m["quantity"]
+        if m["ratio"] is not None and (q not in worst or m["ratio"] > worst[q]["ratio"]):
+            worst[q] = m
+    with open(os.path.join(out, "parity_margins.json"), "w") as f:
+        json.dump({"worst_by_quantity": worst, "cases": _MARGINS}, f, indent=1)
+
+
 def gpu_available():
     try:
         import torch

@@ -13,12 +13,12 @@ import os
 import numpy as np
 import pytest
 
-from conftest import DANGO, FINAL1_CAMERA, GOLDEN, final1_scene, gpu_available, load_png
+from conftest import DANGO, FINAL1_CAMERA, GOLDEN, final1_scene, gpu_available, load_png, record_margin
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
 
 FWD_MAX, FWD_MEAN = 1e-3, 1e-5
-GRAD_TOL = {"centers": 3e-3, "radius": 3e-3, "colors": 3e-3, "light_dir": 1e-2, "ambient": 3e-3}
+GRAD_TOL = {"centers": 3e-3, "radius": 3e-3, "colors": 3e-3, "light_dir": 3e-3, "ambient": 3e-3}
 
 
 @pytest.fixture(scope="module")
@@ -49,6 +49,8 @@ def scene_dev(rm, sc):
 def check_fwd(got, ref):
     e = np.abs(got.astype(np.float64) - ref)
     assert np.isfinite(got).all()
+    record_margin("fwd_max", e.max(), FWD_MAX)
+    record_margin("fwd_mean", e.mean(), FWD_MEAN)
     assert e.max() <= FWD_MAX and e.mean() <= FWD_MEAN, (e.max(), e.mean())
 
 
@@ -58,6 +60,7 @@ def check_grads(got, ref, scale=1.0):
         b = ref[key].reshape(-1)
         bound = tol * max(np.abs(b).max(), 1e-12) * scale
         err = np.abs(a - b).max()
+        record_margin("grad_" + key, err, bound)
         assert err <= bound, (key, err, bound, np.abs(b).max())
 
 

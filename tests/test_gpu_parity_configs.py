@@ -14,17 +14,17 @@ scene.rs:60-128, sdf.rs:30-44 and training.rs:17-34).
   * recovery of the cost-ordered dispatch from list counts a failed launch left uncleared.
 
 Tolerances are the ones of tests/test_gpu_parity.py (forward max 1e-3 / mean 1e-5 linear RGB,
-gradients 3e-3 of the largest fp64 component per group, light_dir 1e-2), except where stated.
+gradients 3e-3 of the largest fp64 component per group, light_dir included), except where stated.
 """
 import numpy as np
 import pytest
 
-from conftest import gpu_available
+from conftest import gpu_available, record_margin
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
 
 FWD_MAX, FWD_MEAN = 1e-3, 1e-5
-GRAD_TOL = {"centers": 3e-3, "radius": 3e-3, "colors": 3e-3, "light_dir": 1e-2, "ambient": 3e-3}
+GRAD_TOL = {"centers": 3e-3, "radius": 3e-3, "colors": 3e-3, "light_dir": 3e-3, "ambient": 3e-3}
 KEYS = ("centers", "colors", "radius", "light_dir", "ambient")
 
 
@@ -57,6 +57,8 @@ def scene_dev(render, sc, color_f16=False):
 def check_fwd(got, ref, fmax=FWD_MAX, fmean=FWD_MEAN):
     e = np.abs(got.astype(np.float64) - ref)
     assert np.isfinite(got).all()
+    record_margin("fwd_max", e.max(), fmax)
+    record_margin("fwd_mean", e.mean(), fmean)
     assert e.max() <= fmax and e.mean() <= fmean, (e.max(), e.mean())
 
 
@@ -66,6 +68,7 @@ def check_grads(got, ref, scale=1.0):
         b = np.asarray(ref[key]).reshape(-1)
         bound = tol * max(np.abs(b).max(), 1e-12) * scale
         err = np.abs(a - b).max()
+        record_margin("grad_" + key, err, bound)
         assert err <= bound, (key, err, bound, np.abs(b).max())
 
 
