@@ -302,11 +302,13 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
       if (comm && (rc = comm->all_reduce_sum(comm->state, d_grad.f(), (int64_t)np + 1, g.stream)) != RMH_OK)
         return fail(rc, "all-reduce of the gradient (stage %d, step %d): %s", stage, step, rmh_last_error());
       const double lr = step > cfg->steps_per_stage / 2 ? base_lr * 0.2 : base_lr;  // train.rs:193-197
-      RMCHK(g.ctx, rm_optimizer_step(g.ctx, d_raw.f(), d_grad.f(), d_m.f(), d_v.f(), M, step, (float)lr,
-                                     cfg->weight_decay, 1, d_loss + 1, d_act.f()));
-      ++steps_done;
       const bool last = stage == cfg->stages - 1 && step == cfg->steps_per_stage;
-      if ((verbose && step % cfg->log_every == 0) || last) {
+      const bool read_loss = (verbose && step % cfg->log_every == 0) || last;
+      // the penalty share of the loss costs a summation launch: only on the steps that report it
+      RMCHK(g.ctx, rm_optimizer_step(g.ctx, d_raw.f(), d_grad.f(), d_m.f(), d_v.f(), M, step, (float)lr,
+                                     cfg->weight_decay, 1, read_loss ? d_loss + 1 : nullptr, d_act.f()));
+      ++steps_done;
+      if (read_loss) {
         float s[2];
         HIPCHK(hipMemcpyAsync(s, d_loss, sizeof s, hipMemcpyDeviceToHost, g.stream));
         HIPCHK(hipStreamSynchronize(g.stream));
