@@ -157,11 +157,21 @@ def main():
         return
 
     import torch
+    # RM_BENCH_BACKEND=gloo: rehearsal of the N-rank path on fewer GPUs than ranks (ranks share
+    # the devices round-robin; RCCL refuses two ranks on one device). Never a measurement.
+    backend = os.environ.get("RM_BENCH_BACKEND", "nccl")
+    if backend not in ("nccl", "gloo"):
+        raise SystemExit(f"RM_BENCH_BACKEND={backend}: nccl or gloo")
+    if backend == "gloo":
+        local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
 
     from burn_raymarching_amd import model as rmm
     from burn_raymarching_amd import native
@@ -387,7 +397,7 @@ def main():
                        "width": W, "height": H, "spheres": M, "march_steps": S, "smooth_k": K,
                        "views_per_gpu": vpg, "rays_per_step": rays_global, "radius_range": list(rr),
                        "color_storage": args.color_dtype, "sdf_dtype": "f32",
-                       "parallelism": f"views-dp{world}"},
+                       "parallelism": f"views-dp{world}" + ("" if backend == "nccl" else f" ({backend} rehearsal)")},
             "value_median": round(rays_global / (med_ms * 1e-3) / 1e6, 3),
             "ms_per_step_median": round(med_ms, 4),
             "host_submit_ms_per_step": round(host_s / args.steps * 1e3, 4),
