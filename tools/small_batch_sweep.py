@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""Time of the training driver's call -- rm_train_step in ray-array mode (train.rs:169-190 with
+the dataset.rs batch) -- over batch size x march steps at the driver's sphere count, to tell
+per-step latency from work. torch events around 50 calls each, after 10
+warm-up calls; rays from the eye at (0, 0, -2.5) through a 50-degree cone, uniform targets.
+
+    python tools/small_batch_sweep.py [--spheres 9] > gpurun_out/small_batch.json
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--spheres", type=int, default=9)
+    ap.add_argument("--k", type=float, default=20.0)
+    args = ap.parse_args()
+    import torch
+    from burn_raymarching_amd import model, render
+    sc = model.scene_tensors(model.synthetic_scene(args.spheres, 5, radius_range=(0.1, 0.3)))
+    rows = []
+    for n in (4096, 16384, 65536, 262144):
+        rng = np.random.default_rng(n)
+        o = np.tile(np.array([[0.0, 0.0, -2.5]], np.float32), (n, 1))
+        d = rng.normal(size=(n, 3)).astype(np.float32) * np.float32(0.2) + np.array([0, 0, 1], np.float32)
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        t = lambda x: torch.from_numpy(np.ascontiguousarray(x, np.float32)).cuda()  # noqa: E731
+        o_, d_, tg = t(o), t(d), t(rng.uniform(size=(n, 3)))
+        for steps in (10, 20, 40):
+            for _ in range(10):
+                render.train_step(o_, d_, tg, sc, args.k, 0.5, steps)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(50):
+                render.train_step(o_, d_, tg, sc, args.k, 0.5, steps)
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) / 50 * 1e3
+            rows.append({"rays": n, "march_steps": steps, "us_per_call": round(us, 2),
+                         "Mrays_s": round(n / us, 1)})
+            print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
+    print(json.dumps({"spheres": args.spheres, "k": args.k, "rows": rows}))
+
+
+if __name__ == "__main__":
+    main()
