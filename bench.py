@@ -163,6 +163,8 @@ def main():
     if backend not in ("nccl", "gloo"):
         raise SystemExit(f"RM_BENCH_BACKEND={backend}: nccl or gloo")
     if backend == "gloo":
+        if torch.cuda.device_count() == 0:
+            raise SystemExit("bench.py needs a HIP device")
         local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
     dist = None
