@@ -80,6 +80,14 @@ class Scene:
     def march_flags(self) -> int:
         return native.RM_MARCH_COLOR_F16 if self.color_f16 else 0
 
+    def march_for(self, march) -> native.RmMarch:
+        """A copy of `march` whose RM_MARCH_COLOR_F16 bit matches this scene's colour dtype (the
+        caller's struct is never modified: a march shared between an fp16-colour and an fp32
+        scene must not carry the bit from one call into the next)."""
+        m = native.RmMarch.from_buffer_copy(march)
+        m.flags = (m.flags & ~native.RM_MARCH_COLOR_F16) | self.march_flags
+        return m
+
     def c_struct(self) -> RmScene:
         return RmScene(self.centers.data_ptr(), self.colors.data_ptr(), self.radius.data_ptr(),
                        self.light_dir.data_ptr(), self.ambient.data_ptr(), self.num_spheres)
@@ -105,7 +113,7 @@ def render_diff_forward(ray_org, ray_dir, scene: Scene, smooth_k, steps=40, *, n
     t = torch.empty((n,), device=ray_org.device) if return_t else None
     ctx = context(ray_org.device)
     march = native.march_params(steps, smooth_k, normal_eps, color_sharpness, mask_sharpness)
-    march.flags |= scene.march_flags
+    march = scene.march_for(march)
     ctx.check(ctx._lib.rm_render_diff(ctx.handle, _ptr(ray_org), _ptr(ray_dir), n, ctypes.byref(scene.c_struct()),
                                       ctypes.byref(march), _ptr(out), _ptr(t)), "rm_render_diff")
     return (out, t) if return_t else out
@@ -123,7 +131,7 @@ def render_diff_backward(ray_org, ray_dir, scene: Scene, smooth_k, grad_out, ste
     g, cg = _grads_like(scene)
     ctx = context(ray_org.device)
     march = native.march_params(steps, smooth_k, normal_eps, color_sharpness, mask_sharpness)
-    march.flags |= scene.march_flags
+    march = scene.march_for(march)
     ctx.check(ctx._lib.rm_render_diff_backward(ctx.handle, _ptr(ray_org), _ptr(ray_dir), n,
                                                ctypes.byref(scene.c_struct()), ctypes.byref(march), _ptr(grad_out),
                                                _ptr(t_march), ctypes.byref(cg), 0), "rm_render_diff_backward")
@@ -171,7 +179,7 @@ def render_diff_camera(cams, width, height, scene: Scene, smooth_k, steps=40, *,
     t = torch.empty((v * height * width,), device=dev) if return_t else None
     ctx = context(dev)
     march = native.march_params(steps, smooth_k, normal_eps, color_sharpness, mask_sharpness)
-    march.flags |= scene.march_flags
+    march = scene.march_for(march)
     for i in range(0, v, native.RM_MAX_VIEWS_PER_CALL):
         chunk = cams[i:i + native.RM_MAX_VIEWS_PER_CALL]
         off = i * height * width
@@ -194,7 +202,7 @@ def render_diff_backward_camera(cams, width, height, scene: Scene, smooth_k, gra
     g, cg = _grads_like(scene)
     ctx = context(scene.centers.device)
     march = native.march_params(steps, smooth_k)
-    march.flags |= scene.march_flags
+    march = scene.march_for(march)
     ctx.check(ctx._lib.rm_render_diff_backward_camera(ctx.handle, native.cameras(cams), len(cams), width, height,
                                                       ctypes.byref(scene.c_struct()), ctypes.byref(march),
                                                       _ptr(grad_out), _ptr(t_march), ctypes.byref(cg), 0),
@@ -216,7 +224,7 @@ def train_step(ray_org, ray_dir, targets, scene: Scene, smooth_k, progress, step
     out = torch.empty((n, 3), device=ray_org.device) if with_out else None
     ctx = context(ray_org.device)
     march = native.march_params(steps, smooth_k)
-    march.flags |= scene.march_flags
+    march = scene.march_for(march)
     ctx.check(ctx._lib.rm_train_step(ctx.handle, _ptr(ray_org), _ptr(ray_dir), _ptr(targets), n, float(progress),
                                      float(inv_count), ctypes.byref(scene.c_struct()), ctypes.byref(march),
                                      ctypes.byref(cg), _ptr(loss), _ptr(out), 0), "rm_train_step")
@@ -245,7 +253,7 @@ def train_step_camera(cams, width, height, targets, scene: Scene, smooth_k, prog
         loss = torch.zeros((1,), device=scene.centers.device)
     if march is None:
         march = native.march_params(steps, smooth_k)
-    march.flags |= scene.march_flags
+    march = scene.march_for(march)
     ctx.check(ctx._lib.rm_train_step_camera(ctx.handle, native.cameras(cams), len(cams), width, height, _ptr(targets),
                                             float(progress), float(inv_count), ctypes.byref(scene.c_struct()),
                                             ctypes.byref(march), ctypes.byref(cg), _ptr(loss), _ptr(out),

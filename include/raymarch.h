@@ -85,7 +85,8 @@ typedef struct rm_march {
 /* Disable the escaped-ray early exit: by default a wave stops marching once all its rays
  * recede from the scene's bounding sphere at a distance where the silhouette mask is exactly
  * 0 in fp32 (their outputs and gradient terms are then exactly 0, as the full computation
- * gives). Set for A/B timing; t_march and debug outputs disable it automatically. */
+ * gives). Set for A/B timing; t_march and debug outputs disable it automatically (rays that
+ * provably escape still step by the escape bound, see t_march below). */
 #define RM_MARCH_NO_EARLY_EXIT 4
 /* Camera mode with 16x16 tiles and whole views per launch: dispatch the ray blocks in launch
  * order instead of centre-out (tiles nearest the image centre first, views interleaved, so the
@@ -162,7 +163,13 @@ int rm_reserve(rm_context* ctx, int64_t max_rays, int32_t max_spheres);
 /* ---- forward: renderer_diff.rs:6-91 --------------------------------------- */
 /* out [N,3] receives render_diff(ray_org, ray_dir, scene..., smooth_k).
  * t_march (nullable) [N] receives the detached march distance t after `steps`
- * steps (renderer_diff.rs:20-26), which rm_render_diff_backward can reuse. */
+ * steps (renderer_diff.rs:20-26), which rm_render_diff_backward can reuse. For a ray that
+ * provably escapes the scene -- receding from its bounding sphere so far that the silhouette
+ * mask, out and every gradient term are exactly 0 in fp32 -- the march continues with steps
+ * of that escape bound (|p - c| - R - ln(M)/k, never longer than the soft-min step), so its
+ * t_march is at most the reference's t and already past the distance where the mask is 0;
+ * every other ray's t_march is the reference march to fp32 rounding. Either t gives the same
+ * out and gradients. */
 int rm_render_diff(rm_context* ctx, const float* ray_org, const float* ray_dir, int64_t num_rays,
                    const rm_scene* scene, const rm_march* march, float* out, float* t_march);
 /* Camera mode: rays of `num_views` cameras at width x height generated in-kernel;

@@ -88,3 +88,29 @@ def test_forward_backward_and_render_identical(mods, monkeypatch):
     monkeypatch.setenv("RM_NO_EARLY_EXIT", "0")
     st = _stats(render, lambda: render.render_diff_camera(cams, 64, 64, sc, 32.0, 32, return_t=True))
     assert st["waves_exited"] == 0
+
+
+def test_t_march_contract_against_oracle(mods, oracle):
+    """t_march (include/raymarch.h): the reference march t (renderer_diff.rs:20-26) to fp32
+    rounding for every ray whose mask is not provably 0; a ray that provably escapes steps by the
+    escape bound, so its t is at most the reference's and its out is exactly 0. Both t give the
+    same image (the saved-t backward is bit-exact: test_gpu_parity.py)."""
+    torch, model, render = mods
+    sc_np = model.synthetic_scene(48, 8)
+    cam = model.ring_cameras(10)[2]
+    o, d = oracle.camera_rays(40, 40, *cam, precision="f32")
+    s = model.scene_tensors(sc_np, "cuda")
+    dev = lambda x: torch.from_numpy(np.ascontiguousarray(x, np.float32)).cuda()  # noqa: E731
+    out, t = render.render_diff_forward(dev(o), dev(d), s, 32.0, 40, return_t=True)
+    ref, t_ref = oracle.render_diff(o.astype(np.float64), d.astype(np.float64), sc_np, 40, 32.0, precision="f64",
+                                    with_t=True)
+    t_gpu = t.cpu().numpy().astype(np.float64)
+    out_gpu = out.cpu().numpy()
+    t_ref = np.asarray(t_ref, np.float64).reshape(-1)
+    close = np.abs(t_gpu - t_ref) <= 1e-3 * np.maximum(1.0, np.abs(t_ref))
+    bounded = (t_gpu <= t_ref * (1 + 1e-5) + 1e-4) & np.all(out_gpu == 0.0, axis=1)
+    assert np.all(close | bounded), np.flatnonzero(~(close | bounded))[:8]
+    assert close.sum() > 0 and np.isfinite(t_gpu).all()
+    # where the ray still sees the scene (reference mask not negligible) t is the reference's
+    seen = np.abs(ref).max(axis=1) > 1e-6
+    assert np.all(close[seen])

@@ -13,18 +13,18 @@ scene.rs:60-128, sdf.rs:30-44 and training.rs:17-34).
     spheres and 128 steps;
   * recovery of the cost-ordered dispatch from list counts a failed launch left uncleared.
 
-Tolerances are the ones of tests/test_gpu_parity.py (forward max 1e-3 / mean 1e-5 linear RGB,
-gradients 3e-3 of the largest fp64 component per group, light_dir included), except where stated.
+Tolerances are the ones of tests/test_gpu_parity.py (forward max 1e-3 / mean 1e-5 linear RGB;
+gradients by conftest.check_grads: 3e-3 of the largest fp64 component per group, relative L2 and
+per-element relative bounds for the per-sphere groups), except where stated.
 """
 import numpy as np
 import pytest
 
-from conftest import gpu_available, record_margin
+from conftest import check_grads, gpu_available, record_margin
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
 
 FWD_MAX, FWD_MEAN = 1e-3, 1e-5
-GRAD_TOL = {"centers": 3e-3, "radius": 3e-3, "colors": 3e-3, "light_dir": 3e-3, "ambient": 3e-3}
 KEYS = ("centers", "colors", "radius", "light_dir", "ambient")
 
 
@@ -60,16 +60,6 @@ def check_fwd(got, ref, fmax=FWD_MAX, fmean=FWD_MEAN):
     record_margin("fwd_max", e.max(), fmax)
     record_margin("fwd_mean", e.mean(), fmean)
     assert e.max() <= fmax and e.mean() <= fmean, (e.max(), e.mean())
-
-
-def check_grads(got, ref, scale=1.0):
-    for key, tol in GRAD_TOL.items():
-        a = host(got[key]).reshape(-1).astype(np.float64)
-        b = np.asarray(ref[key]).reshape(-1)
-        bound = tol * max(np.abs(b).max(), 1e-12) * scale
-        err = np.abs(a - b).max()
-        record_margin("grad_" + key, err, bound)
-        assert err <= bound, (key, err, bound, np.abs(b).max())
 
 
 def cam_rays(oracle, cams, width, height):
@@ -110,7 +100,7 @@ def test_bench_workload_train_step_full_views(rm, oracle):
     loss, g, out = runs[2]
     check_fwd(out, out_ref)
     assert abs(loss[0] - loss_ref) <= 1e-4 * abs(loss_ref), (loss[0], loss_ref)
-    check_grads({k: torch.from_numpy(v) for k, v in g.items()}, g_ref)
+    check_grads(g, g_ref, mode="train")
 
 
 @pytest.mark.parametrize("mode", ["forward", "backward", "train"])
@@ -137,7 +127,7 @@ def test_config2_s64(rm, oracle, mode):
             loss, g, _ = render.train_step_camera(cams, W, H, dev(targets), s, K, 0.25, S)
         out_ref, loss_ref, g_ref = oracle.train_step(o64, d64, targets.astype(np.float64), sc, S, K, 0.25)
         assert abs(host(loss)[0] - loss_ref) <= 1e-4 * abs(loss_ref)
-        check_grads(g, g_ref)
+        check_grads(g, g_ref, mode="train")
 
 
 @pytest.mark.parametrize("flag", ["RM_VALU_ONLY", "RM_FORCE_MAX_SHIFT"])
@@ -167,7 +157,7 @@ def test_forced_march_paths(rm, oracle, monkeypatch, flag, steps):
     loss, gt, _ = render.train_step(dev(o), dev(d), dev(targets), s, K, 0.75, steps)
     _, loss_ref, g_ref = oracle.train_step(o64, d64, targets.astype(np.float64), sc, steps, K, 0.75)
     assert abs(host(loss)[0] - loss_ref) <= 1e-4 * abs(loss_ref)
-    check_grads(gt, g_ref)
+    check_grads(gt, g_ref, mode="train")
 
 
 def _round_f16(sc):
@@ -209,7 +199,7 @@ def test_color_f16_config4(rm, oracle, mode):
         loss, g, _ = render.train_step_camera(cams, W, H, dev(targets), s, K, 0.5, S)
         _, loss_ref, g_ref = oracle.train_step(o64, d64, targets.astype(np.float64), sc16, S, K, 0.5)
         assert abs(host(loss)[0] - loss_ref) <= 1e-4 * abs(loss_ref)
-        check_grads(g, g_ref)
+        check_grads(g, g_ref, mode="train")
 
 
 def test_color_f16_full_size_properties(rm):

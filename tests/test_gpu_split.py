@@ -15,12 +15,11 @@ Tolerances as in tests/test_gpu_parity.py.
 import numpy as np
 import pytest
 
-from conftest import gpu_available, record_margin
+from conftest import check_grads, gpu_available, record_margin
 
 pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
 
 FWD_MAX, FWD_MEAN = 1e-3, 1e-5
-GRAD_TOL = {"centers": 3e-3, "radius": 3e-3, "colors": 3e-3, "light_dir": 3e-3, "ambient": 3e-3}
 KEYS = ("centers", "colors", "radius", "light_dir", "ambient")
 
 
@@ -49,15 +48,6 @@ def check_fwd(got, ref):
     record_margin("fwd_max", e.max(), FWD_MAX)
     record_margin("fwd_mean", e.mean(), FWD_MEAN)
     assert e.max() <= FWD_MAX and e.mean() <= FWD_MEAN, (e.max(), e.mean())
-
-
-def check_grads(got, ref):
-    for key, tol in GRAD_TOL.items():
-        a = host(got[key]).reshape(-1).astype(np.float64)
-        b = np.asarray(ref[key]).reshape(-1)
-        bound = tol * max(np.abs(b).max(), 1e-12)
-        record_margin("grad_" + key, np.abs(a - b).max(), bound)
-        assert np.abs(a - b).max() <= bound, (key, np.abs(a - b).max(), bound)
 
 
 def cam_rays(oracle, cams, w, h):
@@ -91,7 +81,7 @@ def test_split_against_oracle(rm, oracle, monkeypatch, m):
         loss, gt, _ = render.train_step_camera(cams, W, H, dev(targets), s, K, 0.4, S)
     _, loss_ref, g_ref = oracle.train_step(o64, d64, targets.astype(np.float64), sc, S, K, 0.4)
     assert abs(host(loss)[0] - loss_ref) <= 1e-4 * abs(loss_ref)
-    check_grads(gt, g_ref)
+    check_grads(gt, g_ref, mode="train")
 
 
 def _train(render, native, cams, w, h, tg, s, k, steps, flags=0):

@@ -141,3 +141,36 @@ def test_penalty_and_adam_reference_formulas():
     loss = ad.compute_loss(raw, out, torch.zeros_like(out), 0.5)
     loss.backward()
     assert torch.isfinite(raw["centers"].grad).all()
+
+
+def test_fp32_gradient_error_within_gpu_bounds(oracle):
+    """The relative-L2 and per-element gradient bounds of conftest.check_grads are set from the
+    fp32 reference-order oracle's own error against the fp64 oracle: the reference's op order in
+    fp32 must pass them at the -m gpu cases it can run (backward cases of test_gpu_parity.py;
+    a configs[2]-shaped train step, 256 spheres / 64 steps, on a 64x64 view)."""
+    from burn_raymarching_amd import model
+    from conftest import PER_SPHERE, REL_ELEM, REL_L2, grad_errors
+
+    def within(g32, g64, mode):
+        for key in PER_SPHERE:
+            _, rl2, tiers = grad_errors(g32[key], g64[key])
+            assert rl2 <= REL_L2[mode], (mode, key, rl2)
+            for (floor, err), (_, bound) in zip(tiers, REL_ELEM[mode]):
+                assert err <= bound, (mode, key, floor, err)
+
+    for width, m, steps, k, seed in [(64, 8, 16, 32.0, 0), (64, 8, 40, 5.0, 1), (48, 64, 32, 32.0, 2),
+                                     (40, 300, 16, 32.0, 3)]:
+        sc = model.synthetic_scene(m, seed)
+        eye, tgt, fov = model.ring_cameras(7)[seed % 7]
+        o, d = oracle.camera_rays(width, width, eye, tgt, fov, precision="f32")
+        g = np.random.default_rng(seed + 10).normal(size=o.shape).astype(np.float32)
+        g64 = oracle.render_diff_backward(o.astype(np.float64), d.astype(np.float64), sc, steps, k,
+                                          g.astype(np.float64), precision="f64")
+        within(oracle.render_diff_backward(o, d, sc, steps, k, g, precision="f32"), g64, "bwd")
+    sc = model.synthetic_scene(256, 2)
+    o, d = oracle.camera_rays(64, 64, *model.ring_cameras(10, offset=3)[0], precision="f32")
+    o64, d64 = o.astype(np.float64), d.astype(np.float64)
+    tg = oracle.render_diff(o64, d64, model.synthetic_scene(256, 3), 64, 32.0).astype(np.float32)
+    _, _, g64 = oracle.train_step(o64, d64, tg.astype(np.float64), sc, 64, 32.0, 0.25)
+    _, _, g32 = oracle.train_step(o, d, tg, sc, 64, 32.0, 0.25, precision="f32")
+    within(g32, g64, "train")
