@@ -9,9 +9,13 @@ HIP path, per rank:
   all_reduce(grads) [N > 1]  (RCCL over xGMI; 7M+5 floats: gradient + loss)
   rm_optimizer_step          (activation chain rule + training.rs penalties + Burn Adam, which
                               also writes the activated parameters of the next step)
-Views shard across ranks (weak scaling: every rank renders its own 10 views of 512x512 per step).
-value = rays of all ranks * K / max-over-ranks wall time of the K timed steps (barrier +
-synchronize on both sides). `value_median` / `ms_per_step_median` use the median over the K
+Views shard across ranks. Default: STRONG scaling -- a step covers --global-views 80 views of
+512x512 (a ring of 80 cameras) in all, split into contiguous parts over the N ranks (80 on one
+GPU, 10 per GPU on 8), so the total work per step is fixed as N grows; a rank issues its views in
+calls of up to 16 (one launch each), every call slot on its own rm_context so that its
+cost-ordered dispatch comes from the same views' previous step. `--views-per-gpu V` alone selects
+weak scaling (V views per rank per step). value = rays of all ranks * K / max-over-ranks wall time
+of the K timed steps (barrier + synchronize on both sides). `value_median` / `ms_per_step_median` use the median over the K
 steps of the per-step hipEvent time (max over ranks per step).
 
 `--gpus N` without WORLD_SIZE in the environment launches N rank processes itself (one per
@@ -59,6 +63,8 @@ PEAK_FP32_TFLOPS = 157.3   # MI355X_MICROARCH.md chip table (vector fp32, spec)
 PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 FLOP_PER_EVAL = 16         # SURVEY.md §8d canonical count (sqrt and exp counted as 1)
 BYTES_PER_RAY_CAMERA = 24  # SURVEY.md §8d algorithmic HBM bytes per ray, camera mode
+DEFAULT_GLOBAL_VIEWS = 80  # strong scaling: 80 views per step = 10 per GPU at N = 8
+MAX_RAYS_PER_CALL = 16 * 512 * 512  # one launch of 256-ray blocks (kMaxBlocksPerLaunch)
 
 
 def parse():
@@ -71,11 +77,15 @@ def parse():
     ap.add_argument("--spheres", type=int, default=256)
     ap.add_argument("--march-steps", type=int, default=32)
     ap.add_argument("--smooth-k", type=float, default=32.0)
-    ap.add_argument("--views-per-gpu", type=int, default=10,
-                    help="512x512 views per GPU per step: 10 = the whole 10-camera ring of BASELINE configs[1-2] "
-                         "= 2,621,440 rays = 10240 ray blocks in one launch (the once-per-launch ramp-down and "
-                         "the per-step O(M) kernels are amortised); at 8 GPUs a step covers 80 views")
-    ap.add_argument("--ring", type=int, default=10, help="cameras on the target ring")
+    ap.add_argument("--global-views", type=int, default=None,
+                    help="strong scaling (the default, %d views): views per step over ALL ranks, split into "
+                         "contiguous parts over the ranks" % DEFAULT_GLOBAL_VIEWS)
+    ap.add_argument("--views-per-gpu", type=int, default=None,
+                    help="weak scaling: views per GPU per step (e.g. 10 = the 10-camera ring of BASELINE "
+                         "configs[1-2] = 2,621,440 rays in one launch); exclusive with --global-views")
+    ap.add_argument("--ring", type=int, default=10, help="cameras on the target ring (at least the views of a step)")
+    ap.add_argument("--dump-grad", default=None,
+                    help="rank 0 saves the all-reduced [gradient | loss] of step 0 here (.npy; rehearsal tests)")
     ap.add_argument("--radius-range", type=float, nargs=2, default=None,
                     help="activated radii U[lo, hi] of the synthetic scenes (default per SURVEY.md 8d: "
                          "0.03-0.12 up to 256 spheres, 0.02-0.06 up to 1024, 0.01-0.04 beyond)")
@@ -94,7 +104,14 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline: repeat the sample this long")
     ap.add_argument("--skip-escaped", choices=["on", "off"], default="off",
                     help="RM_MARCH_SKIP_ESCAPED: skip ray blocks that provably leave the scene (exact)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.global_views is not None and args.views_per_gpu is not None:
+        ap.error("--global-views (strong scaling) and --views-per-gpu (weak scaling) are exclusive")
+    if args.global_views is None and args.views_per_gpu is None:
+        args.global_views = DEFAULT_GLOBAL_VIEWS
+    if args.global_views is not None and args.global_views < args.gpus:
+        ap.error(f"--global-views {args.global_views} < --gpus {args.gpus}: every rank needs a view")
+    return args
 
 
 def _free_port() -> int:
@@ -172,6 +189,15 @@ def main():
         import torch.distributed as dist
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            # the measured run must be what it claims: --gpus ranks, each on its own device
+            props = torch.cuda.get_device_properties(local)
+            me = (socket.gethostname(), str(props.uuid), f"{props.pci_domain_id}:{props.pci_bus_id}:{props.pci_device_id}")
+            every = [None] * world
+            dist.all_gather_object(every, me)
+            if dist.get_world_size() != args.gpus or len(set(every)) != world:
+                print(f"error: rank {rank}: world {dist.get_world_size()} for --gpus {args.gpus}, devices {every}",
+                      file=sys.stderr, flush=True)
+                sys.exit(3)
         else:
             dist.init_process_group("gloo")
 
@@ -181,19 +207,24 @@ def main():
     from burn_raymarching_amd.parallel import Shard, ViewShardedStep
 
     W, H, M, S, K = args.width, args.height, args.spheres, args.march_steps, args.smooth_k
-    vpg = args.views_per_gpu
-    if not 1 <= vpg <= native.RM_MAX_VIEWS_PER_CALL:
+    strong = args.global_views is not None
+    if not strong and not 1 <= args.views_per_gpu <= native.RM_MAX_VIEWS_PER_CALL:
         raise SystemExit("--views-per-gpu must be in 1..16")
     npix = W * H
+    shard = Shard(rank, world, 0 if strong else args.views_per_gpu, 1, args.global_views or 0)
+    vpg = shard.count()  # this rank's views per step
     rays_per_rank = vpg * npix
-    rays_global = rays_per_rank * world
+    rays_global = shard.views_total * npix
+    # views per train call (one launch of up to 16 views / 4M rays each)
+    views_per_call = max(1, min(native.RM_MAX_VIEWS_PER_CALL, MAX_RAYS_PER_CALL // npix))
 
     # ---- synthetic scene, targets, optimizer --------------------------------------------
     rr = tuple(args.radius_range) if args.radius_range else (
         (0.03, 0.12) if M <= 256 else ((0.02, 0.06) if M <= 1024 else (0.01, 0.04)))
     sc0 = rmm.synthetic_scene(M, seed=0, radius_range=rr)
     sc1 = rmm.synthetic_scene(M, seed=1, radius_range=rr)
-    ring = max(args.ring, world * vpg)
+    ring = max(args.ring, shard.views_total)
+    shard.ring = ring
     cams = rmm.ring_cameras(ring)
     tgt_scene = rmm.scene_tensors(sc1)
     targets = torch.empty((ring, npix, 3), device="cuda")
@@ -204,7 +235,11 @@ def main():
                                           sc0["ambient"], color_dtype=args.color_dtype)
     opt = rmm.Adam(model, weight_decay=1e-5, with_penalties=True)
     march = native.march_params(S, K, skip_escaped=args.skip_escaped == "on")
-    ctx = rmr.context()
+    # one rm_context per call slot of a step (same stream): each keeps the cost-ordered dispatch
+    # state of the views it trains every step
+    ctxs = [rmr.context()] + [native.Context(torch.cuda.current_device(), rmr.context().stream)
+                              for _ in range(1, (vpg + views_per_call - 1) // views_per_call)]
+    ctx = Contexts(ctxs)
     total_steps = args.warmup + args.steps
     progress = {"i": 0}
 
@@ -213,21 +248,26 @@ def main():
     targets2 = torch.cat([targets, targets])
 
     def step_fn(views, inv_count, grads_out, loss_out):
-        # rm_train_step_camera over this rank's views (fused forward + loss seed + backward)
+        # rm_train_step_camera over this rank's views (fused forward + loss seed + backward), in
+        # calls of up to views_per_call views; the later calls add into the gradient and loss
         first = views[0]
         assert views == [(first + j) % ring for j in range(len(views))]
-        tg = targets2[first:first + len(views)]
-        rmr.train_step_camera([cams[j] for j in views], W, H, tg.view(-1, 3), model.scene(), K,
-                              progress=min(progress["i"] / total_steps, 1.0), steps=S, inv_count=inv_count,
-                              grads_packed=grads_out, loss=loss_out, march=march)
+        for c, c0 in enumerate(range(0, len(views), views_per_call)):
+            part = views[c0:c0 + views_per_call]
+            tg = targets2[part[0]:part[0] + len(part)]
+            rmr.train_step_camera([cams[j] for j in part], W, H, tg.view(-1, 3), model.scene(), K,
+                                  progress=min(progress["i"] / total_steps, 1.0), steps=S, inv_count=inv_count,
+                                  grads_packed=grads_out, loss=loss_out, march=march, accumulate=c > 0, ctx=ctxs[c])
 
-    dp = ViewShardedStep(Shard(rank, world, vpg, ring), npix, rmm.packed_size(M), "cuda", step_fn,
-                         optim_fn=lambda g: opt.step(g, args.lr))
+    dp = ViewShardedStep(shard, npix, rmm.packed_size(M), "cuda", step_fn, optim_fn=lambda g: opt.step(g, args.lr))
     loss = dp.loss
+    grad0 = []
 
     def step(i):
         progress["i"] = i
         dp(i)
+        if i == 0 and args.dump_grad and not grad0:
+            grad0.append(dp.buf.detach().clone())
 
     for i in range(args.warmup):
         step(i)
@@ -389,15 +429,17 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded scene + targets rendered by the forward kernel)",
-            "config": {"workload": f"train step fwd+bwd, {W}x{H} view(s) per GPU, {M} spheres, {S} march steps, "
-                                   f"k={K:g}, camera mode, Adam"
+            "config": {"workload": (f"train step fwd+bwd, {shard.views_total} {W}x{H} views per step over all GPUs"
+                                    if strong else f"train step fwd+bwd, {vpg} {W}x{H} view(s) per GPU")
+                                   + f", {M} spheres, {S} march steps, k={K:g}, camera mode, Adam"
                                    + (", fp16 colour / fp32 SDF" if args.color_dtype == "f16" else ""),
                        "width": W, "height": H, "spheres": M, "march_steps": S, "smooth_k": K,
-                       "views_per_gpu": vpg, "rays_per_step": rays_global, "radius_range": list(rr),
+                       "views_per_gpu": vpg, "global_views": shard.views_total, "views_per_call": views_per_call,
+                       "ring": ring, "rays_per_step": rays_global, "radius_range": list(rr),
                        "color_storage": args.color_dtype, "sdf_dtype": "f32",
                        "parallelism": f"views-dp{world}" + ("" if backend == "nccl" else f" ({backend} rehearsal)")},
             "value_median": round(rays_global / (med_ms * 1e-3) / 1e6, 3),
@@ -415,8 +457,40 @@ def main():
             "finite": finite,
         }
         print(json.dumps(line), flush=True)
+        if args.dump_grad and grad0:
+            np.save(args.dump_grad, grad0[0].cpu().numpy())
     if dist is not None:
         dist.destroy_process_group()
+
+
+class Contexts:
+    """The rm_contexts of a step's call slots, timed and counted together."""
+
+    def __init__(self, ctxs):
+        self.ctxs = ctxs
+
+    def timing(self, enable=True):
+        for c in self.ctxs:
+            c.timing(enable)
+
+    def collect_timing(self, reset=True):
+        ms, n = 0.0, 0
+        for c in self.ctxs:
+            a, b = c.collect_timing(reset=reset)
+            ms += a
+            n += b
+        return ms, n
+
+    def stats(self, enable=True):
+        for c in self.ctxs:
+            c.stats(enable)
+
+    def collect_stats(self, reset=True):
+        tot = {}
+        for c in self.ctxs:
+            for k, v in c.collect_stats(reset=reset).items():
+                tot[k] = tot.get(k, 0) + v
+        return tot
 
 
 def cpu_baseline(args, sc0, sc1, cam, W, H, M, S, K):

@@ -19,15 +19,41 @@ import torch
 
 @dataclass
 class Shard:
+    """Which views a rank renders at a step.
+
+    Weak scaling (global_views == 0): every rank renders `views_per_rank` views per step, so the
+    step covers views_per_rank * world views. Strong scaling (global_views = V > 0): a step covers
+    V views in all, split into contiguous parts over the ranks (V // world each, the first
+    V % world ranks one more), so the work per step is fixed as the world grows."""
     rank: int
     world: int
     views_per_rank: int
     ring: int  # number of cameras in the rotation
+    global_views: int = 0
+
+    def count(self, rank: int | None = None) -> int:
+        """Views per step of `rank` (default: this rank)."""
+        r = self.rank if rank is None else rank
+        if self.global_views <= 0:
+            return self.views_per_rank
+        base, extra = divmod(self.global_views, self.world)
+        return base + (1 if r < extra else 0)
+
+    @property
+    def views_total(self) -> int:
+        """Views per step over all ranks."""
+        return self.global_views if self.global_views > 0 else self.views_per_rank * self.world
 
     def views(self, step: int) -> list[int]:
         """Views of this rank at `step`: a contiguous block of the ring, rotating every step."""
-        first = ((step * self.world + self.rank) * self.views_per_rank) % self.ring
-        return [(first + j) % self.ring for j in range(self.views_per_rank)]
+        if self.global_views <= 0:
+            first = ((step * self.world + self.rank) * self.views_per_rank) % self.ring
+            n = self.views_per_rank
+        else:
+            start = sum(self.count(r) for r in range(self.rank))
+            first = (step * self.global_views + start) % self.ring
+            n = self.count()
+        return [(first + j) % self.ring for j in range(n)]
 
 
 class ViewShardedStep:
@@ -43,7 +69,7 @@ class ViewShardedStep:
                  step_fn: Callable[[Sequence[int], float, torch.Tensor, torch.Tensor], None],
                  optim_fn: Callable[[torch.Tensor], None] | None = None, group=None):
         self.shard = shard
-        self.rays_global = rays_per_view * shard.views_per_rank * shard.world
+        self.rays_global = rays_per_view * shard.views_total
         self.inv_count = 1.0 / (3.0 * self.rays_global)
         # one buffer, one collective: [packed gradient | loss sum]
         self.buf = torch.zeros(num_params + 1, device=device)
