@@ -38,7 +38,7 @@ def _stale(target: str, sources) -> bool:
 
 def build_lib(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIBDIR, exist_ok=True)
-    srcs = [os.path.join(CSRC, "rm_kernels.hip"), os.path.join(CSRC, "rm_device.h"),
+    srcs = [os.path.join(CSRC, "rm_kernels.hip"), os.path.join(CSRC, "rm_device.h"), os.path.join(CSRC, "rm_small.h"),
             os.path.join(ROOT, "include", "raymarch.h")]
     if force or _stale(LIB, srcs):
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",

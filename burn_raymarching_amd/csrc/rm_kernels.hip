@@ -2669,6 +2669,8 @@ __global__ void rm_sum_small(const float* __restrict__ parts, int n, float* __re
   }
 }
 
+#include "rm_small.h"
+
 }  // namespace rm
 
 // =======================================================================================
@@ -2686,6 +2688,7 @@ struct rm_context {
   unsigned long long* stats_dev = nullptr;  // escaped-block counter (rm_stats_enable)
   int* esc_flags = nullptr;                 // per-block escape flags, kMaxBlocksPerLaunch ints
   void* rec = nullptr;                      // sphere records of the current call (rm_prep_kernel)
+  unsigned* arrivals = nullptr;             // rm_small_kernel's arrival counter (zero between launches)
   size_t rec_bytes = 0;
   long long stats_blocks = 0;               // ray blocks launched while stats are on
   long long stats_waves = 0;                // their ray waves (a split block holds one)
@@ -2888,6 +2891,129 @@ struct Call {
   int accumulate = 0;
 };
 
+FinalArgs final_args(const Call& c, bool first) {
+  const rm_grads* gp = c.grads;
+  FinalArgs fa;
+  fa.light_dir = c.scene->light_dir;
+  fa.gc = gp->centers;
+  fa.gcol = gp->colors;
+  fa.gr = gp->radius;
+  fa.gld = gp->light_dir;
+  fa.gamb = gp->ambient;
+  fa.loss_sum = c.mode == kTrain ? c.loss_sum : nullptr;
+  fa.accumulate = first ? c.accumulate : 1;
+  return fa;
+}
+
+// The fixed-order cross-block reduction of a launch's nb partial records (a.partials) and the
+// gradient scatter into the caller's layout (rm_reduce_partials + rm_finalize_grads).
+int reduce_and_finalize(rm_context* ctx, const Call& c, const KArgs& a, long long nb, bool first) {
+  const int nblocks = (int)nb;
+  const int ncols = a.Mpad * 8 + 8;
+  float* S = a.partials + (long long)std::max<long long>(nb, 1) * a.rec;
+  const int segs = kReduceSegs;  // every segment is written (empty ones as 0)
+  const int seg_len = (nblocks + segs - 1) / segs;
+  const int xblocks = (ncols + 255) / 256;
+  hipLaunchKernelGGL(rm_reduce_partials, dim3((unsigned)xblocks, (unsigned)segs), dim3(256), 0, ctx->stream, a.partials,
+                     a.rec, a.M, a.Mpad, nblocks, seg_len, S);
+  RM_HIP(ctx, hipGetLastError());
+  hipLaunchKernelGGL(rm_finalize_grads, dim3((unsigned)((ncols + 63) / 64)), dim3(256), 0, ctx->stream, S, segs, a.M,
+                     a.Mpad, final_args(c, first));
+  RM_HIP(ctx, hipGetLastError());
+  return RM_OK;
+}
+
+// Per-launch timing events (rm_timing_enable): the next pair of the context's pool.
+int next_events(rm_context* ctx, hipEvent_t& ev0, hipEvent_t& ev1) {
+  ev0 = ev1 = nullptr;
+  if (!ctx->timing) return RM_OK;
+  if (ctx->events_used == ctx->events.size()) {
+    std::pair<hipEvent_t, hipEvent_t> pr;
+    RM_HIP(ctx, hipEventCreate(&pr.first));
+    RM_HIP(ctx, hipEventCreate(&pr.second));
+    ctx->events.push_back(pr);
+  }
+  ev0 = ctx->events[ctx->events_used].first;
+  ev1 = ctx->events[ctx->events_used].second;
+  ++ctx->events_used;
+  return RM_OK;
+}
+
+bool env_is(const char* name, char v) {
+  const char* e = std::getenv(name);
+  return e && e[0] == v;
+}
+
+// Small scenes (M <= kSmallMaxM): rm_small_kernel. Taken by default for ray-array calls (the
+// reference training loop's random batches, train.rs:169-199); env RM_SMALL=1 takes it for every
+// eligible call (camera mode too), RM_SMALL=0 never. Not for the renderer.rs mode, the diagnostics
+// or the flags that select the general kernel's march paths for testing.
+bool use_small(const Call& c, int M, long long n) {
+  if (M > kSmallMaxM || n <= 0 || c.mode == kRender || c.dbg) return false;
+  if ((c.march->flags & (RM_MARCH_VALU_ONLY | RM_MARCH_FORCE_MAX_SHIFT | RM_MARCH_SPLIT)) != 0) return false;
+  const char* e = std::getenv("RM_SMALL");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return !c.cam;
+}
+
+template <int MODE, bool CAM>
+void launch_small_m(int M, dim3 grid, hipStream_t st, const KArgs& a, const SmallArgs& sa, hipEvent_t ev0,
+                    hipEvent_t ev1) {
+  if (M <= 8)
+    hipExtLaunchKernelGGL((rm_small_kernel<MODE, CAM, 8>), grid, dim3(kBlock), 0, st, ev0, ev1, 0u, a, sa);
+  else if (M <= 16)
+    hipExtLaunchKernelGGL((rm_small_kernel<MODE, CAM, 16>), grid, dim3(kBlock), 0, st, ev0, ev1, 0u, a, sa);
+  else
+    hipExtLaunchKernelGGL((rm_small_kernel<MODE, CAM, 32>), grid, dim3(kBlock), 0, st, ev0, ev1, 0u, a, sa);
+}
+
+int run_small(rm_context* ctx, const Call& c, KArgs& a, long long n) {
+  const bool has_bwd = c.mode == kBwd || c.mode == kTrain;
+  int rc;
+  if (has_bwd && (rc = ensure_ws(ctx, ws_need(n, a.M))) != RM_OK) return rc;
+  if (!ctx->arrivals) {
+    RM_HIP(ctx, hipMalloc(&ctx->arrivals, 64));
+    RM_HIP(ctx, hipMemsetAsync(ctx->arrivals, 0, 64, ctx->stream));
+  }
+  long long done = 0;
+  bool first = true;
+  while (done < n) {
+    const long long nb = std::min<long long>((n - done + kBlock - 1) / kBlock, max_blocks_per_launch());
+    const long long nr = std::min<long long>(n - done, nb * kBlock);
+    a.ray_begin = done;
+    a.n_rays = nr;
+    a.partials = static_cast<float*>(ctx->ws);
+    SmallArgs sa;
+    std::memset(&sa, 0, sizeof sa);
+    if (has_bwd) sa.fin = final_args(c, first);
+    sa.arrivals = ctx->arrivals;
+    sa.final_in_kernel = has_bwd && nb <= kSmallFinalMaxBlocks && !env_is("RM_SMALL_FINAL", '0') ? 1 : 0;
+    if (ctx->stats_dev) {
+      ctx->stats_blocks += nb;
+      ctx->stats_waves += nb * kWaves;
+    }
+    hipEvent_t ev0, ev1;
+    if ((rc = next_events(ctx, ev0, ev1)) != RM_OK) return rc;
+    const dim3 grid((unsigned)nb);
+    if (c.mode == kFwd) {
+      if (c.cam) launch_small_m<kFwd, true>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
+      else launch_small_m<kFwd, false>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
+    } else if (c.mode == kBwd) {
+      if (c.cam) launch_small_m<kBwd, true>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
+      else launch_small_m<kBwd, false>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
+    } else {
+      if (c.cam) launch_small_m<kTrain, true>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
+      else launch_small_m<kTrain, false>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
+    }
+    RM_HIP(ctx, hipGetLastError());
+    if (has_bwd && !sa.final_in_kernel && (rc = reduce_and_finalize(ctx, c, a, nb, first)) != RM_OK) return rc;
+    done += nr;
+    first = false;
+  }
+  return RM_OK;
+}
+
 template <int MODE>
 void launch_escape(bool cam, dim3 grid, hipStream_t st, const KArgs& a, int* flags) {
   if (cam)
@@ -3012,6 +3138,7 @@ int run(rm_context* ctx, const Call& c) {
     for (int i = 0; i < 3; ++i) a.light_fixed[i] = lv[i] / len;
   }
   a.rec = rec_floats(Mpad);
+  if (use_small(c, M, n)) return run_small(ctx, c, a, n);
   // sphere records of this call (rm_prep_kernel): read by every sweep through scalar loads
   if (n > 0) {
     const int np = Mpad / 2, nprep = (np + 255) / 256;
@@ -3131,18 +3258,8 @@ int run(rm_context* ctx, const Call& c) {
       a.esc_flags = ctx->esc_flags;
     }
     if (nb > 0) {
-      hipEvent_t ev0 = nullptr, ev1 = nullptr;
-      if (ctx->timing) {
-        if (ctx->events_used == ctx->events.size()) {
-          std::pair<hipEvent_t, hipEvent_t> pr;
-          RM_HIP(ctx, hipEventCreate(&pr.first));
-          RM_HIP(ctx, hipEventCreate(&pr.second));
-          ctx->events.push_back(pr);
-        }
-        ev0 = ctx->events[ctx->events_used].first;
-        ev1 = ctx->events[ctx->events_used].second;
-        ++ctx->events_used;
-      }
+      hipEvent_t ev0, ev1;
+      if ((rc = next_events(ctx, ev0, ev1)) != RM_OK) return rc;
       dim3 grid((unsigned)nb);
 #ifdef RM_BLOCK_TRACE
       if (!ctx->btrace)
@@ -3201,47 +3318,14 @@ int run(rm_context* ctx, const Call& c) {
         b.ocnt_z = nullptr;  // cleared by the first launch
         b.olist_r = nullptr;
         b.ocnt_r = nullptr;
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (ctx->timing) {
-          if (ctx->events_used == ctx->events.size()) {
-            std::pair<hipEvent_t, hipEvent_t> pr;
-            RM_HIP(ctx, hipEventCreate(&pr.first));
-            RM_HIP(ctx, hipEventCreate(&pr.second));
-            ctx->events.push_back(pr);
-          }
-          e0 = ctx->events[ctx->events_used].first;
-          e1 = ctx->events[ctx->events_used].second;
-          ++ctx->events_used;
-        }
+        hipEvent_t e0, e1;
+        if ((rc = next_events(ctx, e0, e1)) != RM_OK) return rc;
         if (c.mode == kBwd) launch_ray<kBwd>(c.cam, true, grid, lds, ctx->stream, b, e0, e1);
         else launch_ray<kTrain>(c.cam, true, grid, lds, ctx->stream, b, e0, e1);
         RM_HIP(ctx, hipGetLastError());
       }
     }
-    if (has_bwd) {
-      const int nblocks = (int)nb;
-      const int ncols = Mpad * 8 + 8;
-      float* S = P + (long long)std::max<long long>(nb, 1) * a.rec;
-      const int segs = kReduceSegs;  // every segment is written (empty ones as 0)
-      const int seg_len = (nblocks + segs - 1) / segs;
-      const int xblocks = (ncols + 255) / 256;
-      const rm_grads* gp = c.grads;
-      FinalArgs fa;
-      fa.light_dir = c.scene->light_dir;
-      fa.gc = gp->centers;
-      fa.gcol = gp->colors;
-      fa.gr = gp->radius;
-      fa.gld = gp->light_dir;
-      fa.gamb = gp->ambient;
-      fa.loss_sum = c.mode == kTrain ? c.loss_sum : nullptr;
-      fa.accumulate = first ? c.accumulate : 1;
-      hipLaunchKernelGGL(rm_reduce_partials, dim3((unsigned)xblocks, (unsigned)segs), dim3(256), 0, ctx->stream, P,
-                         a.rec, M, Mpad, nblocks, seg_len, S);
-      RM_HIP(ctx, hipGetLastError());
-      hipLaunchKernelGGL(rm_finalize_grads, dim3((unsigned)((ncols + 63) / 64)), dim3(256), 0, ctx->stream, S, segs, M,
-                         Mpad, fa);
-      RM_HIP(ctx, hipGetLastError());
-    }
+    if (has_bwd && (rc = reduce_and_finalize(ctx, c, a, nb, first)) != RM_OK) return rc;
     done += nr;
     first = false;
   } while (done < n);
@@ -3378,6 +3462,10 @@ void rm_destroy(rm_context* ctx) {
     if (ctx->cont_buf) (void)hipFree(ctx->cont_buf);
     if (ctx->ocnt) (void)hipFree(ctx->ocnt);
     if (ctx->rec) (void)hipFree(ctx->rec);
+  }
+  if (ctx->arrivals) {
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(ctx->arrivals);
   }
   for (auto& pr : ctx->events) {
     (void)hipEventDestroy(pr.first);

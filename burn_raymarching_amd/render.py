@@ -232,9 +232,10 @@ def train_step(ray_org, ray_dir, targets, scene: Scene, smooth_k, progress, step
 
 
 def train_step_camera(cams, width, height, targets, scene: Scene, smooth_k, progress, steps=40, *, inv_count=None,
-                      grads_packed=None, loss=None, out=None, accumulate=False, march=None):
+                      grads_packed=None, loss=None, out=None, accumulate=False, march=None, ctx=None):
     """Camera-mode fused train step. If grads_packed ((7M+4) device tensor) is given the
-    gradients go there in the packed layout; otherwise a dict is returned."""
+    gradients go there in the packed layout; otherwise a dict is returned. ctx: the rm_context
+    to run on (default: the one of torch's current stream)."""
     cams = list(cams)
     if not 1 <= len(cams) <= native.RM_MAX_VIEWS_PER_CALL:
         raise ValueError("1..16 views per call")
@@ -242,7 +243,8 @@ def train_step_camera(cams, width, height, targets, scene: Scene, smooth_k, prog
     targets = _f32(targets, (n, 3), "targets")
     if inv_count is None:
         inv_count = 1.0 / (3.0 * n)
-    ctx = context(scene.centers.device)
+    if ctx is None:
+        ctx = context(scene.centers.device)
     if grads_packed is not None:
         cg = RmGrads()
         ctx._lib.rm_grads_from_packed(_ptr(grads_packed), scene.num_spheres, ctypes.byref(cg))

@@ -1,0 +1,211 @@
+"""The small-scene kernel (rm_small_kernel, M <= 32; csrc/rm_small.h) through the C ABI against the
+fp64 oracle, at the shape of the reference's own training loop: ray-array train steps of a random
+16,384-ray batch drawn from the pixels of several views (dataset.rs:47-82), 7-20 spheres, 40 march
+steps (renderer_diff.rs:20-26), k annealed 5 -> 32 (train.rs:174). Also: every sphere-count bucket
+edge, ragged and multi-launch ray counts (the in-kernel last-block reduction and the partial-record
+path), forward / backward / t_march, fp16 colours, accumulate, camera mode (RM_SMALL=1), bitwise
+determinism, and agreement with the general kernel (RM_SMALL=0). Tolerances: tests/conftest.py."""
+import numpy as np
+import pytest
+
+from conftest import check_grads, gpu_available, record_margin
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(not gpu_available(), reason="needs a HIP device")]
+
+FWD_MAX, FWD_MEAN = 1e-3, 1e-5
+KEYS = ("centers", "colors", "radius", "light_dir", "ambient")
+
+
+@pytest.fixture(scope="module")
+def rm():
+    import torch
+    from burn_raymarching_amd import _build
+    _build.build_lib()
+    from burn_raymarching_amd import model, native, render
+    torch.cuda.init()
+    return render, model, native
+
+
+def dev(x):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(x, np.float32)).cuda()
+
+
+def host(t):
+    return t.detach().float().cpu().numpy()
+
+
+def check_fwd(got, ref):
+    e = np.abs(got.astype(np.float64) - ref)
+    assert np.isfinite(got).all()
+    record_margin("fwd_max", e.max(), FWD_MAX)
+    record_margin("fwd_mean", e.mean(), FWD_MEAN)
+    assert e.max() <= FWD_MAX and e.mean() <= FWD_MEAN, (e.max(), e.mean())
+
+
+def batch(oracle, model, n, seed, views=6, size=96):
+    """n rays drawn uniformly (seeded) from the pixels of `views` ring views, as the dataset's
+    uniform share draws them (dataset.rs:54-61)."""
+    cams = model.ring_cameras(views, offset=seed % 3)
+    rays = [oracle.camera_rays(size, size, *c, precision="f32") for c in cams]
+    o = np.concatenate([r[0] for r in rays])
+    d = np.concatenate([r[1] for r in rays])
+    idx = np.random.default_rng(seed).integers(0, o.shape[0], n)
+    return o[idx], d[idx]
+
+
+def train_scene(model, m, seed):
+    # the reference's scenes after prune/split: a few larger spheres (train.rs:103-126, training.rs:185-222)
+    return model.synthetic_scene(m, seed, radius_range=(0.08, 0.3))
+
+
+@pytest.mark.parametrize("k", [5.0, 32.0])
+@pytest.mark.parametrize("m", [7, 9, 20])
+def test_reference_training_call(rm, oracle, monkeypatch, m, k):
+    """The reference loop's call: rm_train_step on 16,384 random rays, S = 40 (default path)."""
+    render, model, _ = rm
+    monkeypatch.delenv("RM_SMALL", raising=False)
+    n, steps = 16384, 40
+    sc = train_scene(model, m, 30 + m)
+    o, d = batch(oracle, model, n, m)
+    o64, d64 = o.astype(np.float64), d.astype(np.float64)
+    targets = oracle.render_diff(o64, d64, train_scene(model, 5, 7), steps, 32.0)
+    out_ref, loss_ref, g_ref = oracle.train_step(o64, d64, targets, sc, steps, k, 0.4)
+    loss, g, out = render.train_step(dev(o), dev(d), dev(targets), model.scene_tensors(sc), k, 0.4, steps,
+                                     with_out=True)
+    check_fwd(host(out), out_ref)
+    assert abs(host(loss)[0] - loss_ref) <= 1e-4 * abs(loss_ref) + 1e-3
+    check_grads(g, g_ref, mode="train")
+
+
+@pytest.mark.parametrize("m", [1, 4, 8, 12, 16, 17, 24, 32])
+@pytest.mark.parametrize("n", [1, 257, 4096])
+def test_bucket_edges_forward_backward(rm, oracle, m, n):
+    render, model, _ = rm
+    sc = model.synthetic_scene(m, m + n)
+    o, d = batch(oracle, model, n, m * 7 + n, views=3, size=48)
+    o64, d64 = o.astype(np.float64), d.astype(np.float64)
+    s = model.scene_tensors(sc)
+    out, t = render.render_diff_forward(dev(o), dev(d), s, 24.0, 20, return_t=True)
+    check_fwd(host(out), oracle.render_diff(o64, d64, sc, 20, 24.0))
+    g = np.random.default_rng(n).normal(size=o.shape)
+    gref = oracle.render_diff_backward(o64, d64, sc, 20, 24.0, g)
+    got = render.render_diff_backward(dev(o), dev(d), s, 24.0, dev(g), 20)
+    if n >= 257:
+        check_grads(got, gref)
+    else:  # one ray: a handful of terms; normwise bound only (relative bounds need a population)
+        for key in KEYS:
+            a, b = host(got[key]).reshape(-1), gref[key].reshape(-1)
+            assert np.abs(a - b).max() <= 3e-3 * max(np.abs(b).max(), 1e-12), key
+    # the saved t gives the same gradients bit for bit
+    got_t = render.render_diff_backward(dev(o), dev(d), s, 24.0, dev(g), 20, t_march=t)
+    for key in KEYS:
+        assert np.array_equal(host(got[key]), host(got_t[key])), key
+
+
+@pytest.mark.parametrize("n", [65536, 70000, 300000])
+def test_many_blocks_and_sublaunches(rm, oracle, monkeypatch, n):
+    """> kSmallFinalMaxBlocks blocks: partial records + rm_reduce_partials / rm_finalize_grads;
+    with RM_MAX_BLOCKS_PER_LAUNCH the call splits into launches that accumulate."""
+    render, model, _ = rm
+    if n == 300000:
+        monkeypatch.setenv("RM_MAX_BLOCKS_PER_LAUNCH", "400")
+    sc = train_scene(model, 11, 5)
+    o, d = batch(oracle, model, n, 3, views=8, size=128)
+    o64, d64 = o.astype(np.float64), d.astype(np.float64)
+    targets = oracle.render_diff(o64, d64, train_scene(model, 4, 9), 16, 32.0)
+    out_ref, loss_ref, g_ref = oracle.train_step(o64, d64, targets, sc, 16, 20.0, 0.7)
+    loss, g, out = render.train_step(dev(o), dev(d), dev(targets), model.scene_tensors(sc), 20.0, 0.7, 16,
+                                     with_out=True)
+    check_fwd(host(out), out_ref)
+    assert abs(host(loss)[0] - loss_ref) <= 1e-4 * abs(loss_ref) + 1e-3
+    check_grads(g, g_ref, mode="train")
+
+
+def test_deterministic_and_accumulate(rm, oracle):
+    """Repeated calls are bitwise equal (fixed-order lane / wave / block sums, the last block's
+    reduction included); accumulate = 1 adds exactly the same gradient again (2x, exact)."""
+    import ctypes
+    import torch
+    render, model, native = rm
+    sc = train_scene(model, 13, 1)
+    o, d = batch(oracle, model, 16384, 11)
+    tg = dev(np.random.default_rng(2).uniform(size=o.shape))
+    s = model.scene_tensors(sc)
+    runs = [render.train_step(dev(o), dev(d), tg, s, 12.0, 0.2, 40) for _ in range(3)]
+    for r in runs[1:]:
+        assert torch.equal(r[0], runs[0][0])
+        for key in KEYS:
+            assert torch.equal(r[1][key], runs[0][1][key]), key
+    loss, g, _ = runs[0]
+    g2 = {k: v.clone() for k, v in g.items()}
+    cg = native.RmGrads(*(g2[k].data_ptr() for k in KEYS))
+    l2 = loss.clone()
+    ctx = render.context()
+    march = s.march_for(native.march_params(40, 12.0))
+    od, dd = dev(o), dev(d)  # held: the call reads them asynchronously
+    ctx.check(ctx._lib.rm_train_step(ctx.handle, ctypes.c_void_p(od.data_ptr()), ctypes.c_void_p(dd.data_ptr()),
+                                     ctypes.c_void_p(tg.data_ptr()), 16384, 0.2, 1.0 / (3 * 16384),
+                                     ctypes.byref(s.c_struct()), ctypes.byref(march), ctypes.byref(cg),
+                                     ctypes.c_void_p(l2.data_ptr()), None, 1), "rm_train_step")
+    torch.cuda.synchronize()
+    assert torch.equal(l2, 2.0 * loss)
+    for key in KEYS:
+        assert torch.equal(g2[key], 2.0 * g[key]), key
+
+
+def test_color_f16_small(rm, oracle):
+    """fp16 colours through the small kernel: equal to the fp32 path on the rounded colours."""
+    import torch
+    render, model, _ = rm
+    sc = train_scene(model, 10, 4)
+    o, d = batch(oracle, model, 5000, 4)
+    rounded = dict(sc, colors=sc["colors"].astype(np.float16).astype(np.float32))
+    s16 = render.Scene(dev(sc["centers"]), dev(sc["colors"]).half(), dev(sc["radius"]), dev(sc["light_dir"]),
+                       dev(sc["ambient"]))
+    a = render.render_diff_forward(dev(o), dev(d), s16, 32.0, 40)
+    b = render.render_diff_forward(dev(o), dev(d), model.scene_tensors(rounded), 32.0, 40)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("m", [6, 20])
+def test_camera_mode_small(rm, oracle, monkeypatch, m):
+    """Camera mode through the small kernel (RM_SMALL=1): bit-identical to array mode on the
+    camera.rs rays, and against the oracle."""
+    import torch
+    render, model, _ = rm
+    monkeypatch.setenv("RM_SMALL", "1")
+    sc = train_scene(model, m, 2)
+    cams = model.ring_cameras(3)
+    out = render.render_diff_camera(cams, 48, 32, model.scene_tensors(sc), 32.0, 40)
+    rays = [oracle.camera_rays(48, 32, *c, precision="f32") for c in cams]
+    o = np.concatenate([r[0] for r in rays])
+    d = np.concatenate([r[1] for r in rays])
+    arr = render.render_diff_forward(dev(o), dev(d), model.scene_tensors(sc), 32.0, 40)
+    assert torch.equal(out, arr)
+    check_fwd(host(out), oracle.render_diff(o.astype(np.float64), d.astype(np.float64), sc, 40, 32.0))
+    tg = dev(np.random.default_rng(1).uniform(size=o.shape))
+    _, ga, _ = render.train_step(dev(o), dev(d), tg, model.scene_tensors(sc), 32.0, 0.5, 40)
+    _, gb, _ = render.train_step_camera(cams, 48, 32, tg, model.scene_tensors(sc), 32.0, 0.5, 40)
+    for key in KEYS:
+        a, b = host(ga[key]), host(gb[key])
+        assert np.abs(a - b).max() <= 1e-5 * max(np.abs(a).max(), 1e-12), key
+
+
+def test_small_and_general_kernel_agree(rm, oracle, monkeypatch):
+    """The small kernel and the general kernel (RM_SMALL=0) on the same call: both within the
+    oracle's bounds, and within fp32 rounding of each other."""
+    render, model, _ = rm
+    sc = train_scene(model, 9, 3)
+    o, d = batch(oracle, model, 16384, 5)
+    tg = dev(np.random.default_rng(3).uniform(size=o.shape))
+    res = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("RM_SMALL", flag)
+        loss, g, out = render.train_step(dev(o), dev(d), tg, model.scene_tensors(sc), 24.0, 0.3, 40, with_out=True)
+        res[flag] = (host(loss)[0], {k: host(v) for k, v in g.items()}, host(out))
+    assert abs(res["1"][0] - res["0"][0]) <= 1e-4 * abs(res["0"][0])
+    assert np.abs(res["1"][2] - res["0"][2]).max() <= 1e-3
+    for key in KEYS:
+        a, b = res["1"][1][key], res["0"][1][key]
+        assert np.abs(a - b).max() <= 3e-3 * max(np.abs(b).max(), 1e-12), key

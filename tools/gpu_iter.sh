@@ -1,0 +1,35 @@
+# One GPU iteration: the -m gpu suite (stop at the first failure), then optional steps by name.
+#   bash tools/gpu_iter.sh <tag> [tests] [small] [bench] [train]
+# tests: pytest -m gpu; small: tools/small_batch_sweep.py + its rocprofv3 stats; bench: bench.py
+# + rocprofv3 stats; train: the C++ driver's whole schedule (rm_train) timed. Outputs under
+# gpurun_out/<tag>/. Every GPU step runs under its own time limit; the first failure ends the run.
+set -o pipefail
+export TMPDIR=/tmp
+TAG=${1:-it}
+shift
+O=gpurun_out/$TAG
+mkdir -p $O
+for step in "$@"; do
+  case $step in
+    tests)
+      timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/tests.log 2>&1 \
+        || { echo "tests failed"; tail -40 $O/tests.log; exit 1; }
+      tail -2 $O/tests.log; cp gpurun_out/parity_margins.json $O/ ;;
+    small)
+      timeout -k 10 300 python tools/small_batch_sweep.py > $O/small.json 2> $O/small.err || { tail $O/small.err; exit 1; }
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof_small -o run \
+        -- python3 tools/small_batch_sweep.py > $O/prof_small.log 2>&1 || { tail $O/prof_small.log; exit 1; } ;;
+    bench)
+      timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
+      cat $O/bench.json ;;
+    train)
+      mkdir -p $O/train_out
+      timeout -k 10 300 burn_raymarching_amd/lib/rm_train train --cameras tests/golden/cameras.json --out $O/train_out \
+        --no-previews --log-every 700 > $O/train.log 2>&1 || { tail $O/train.log; exit 1; }
+      tail -4 $O/train.log
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof_train -o run \
+        -- burn_raymarching_amd/lib/rm_train train --cameras tests/golden/cameras.json --out $O/train_out --no-previews \
+        --log-every 0 > $O/prof_train.log 2>&1 || { tail $O/prof_train.log; exit 1; } ;;
+  esac
+done
+echo done
