@@ -2957,15 +2957,21 @@ bool use_small(const Call& c, int M, long long n) {
   return !c.cam;
 }
 
-template <int MODE, bool CAM>
+// rm_small_kernel for M spheres: the bucket of M rounded up to a multiple of 4
+template <int MODE>
 void launch_small_m(int M, dim3 grid, hipStream_t st, const KArgs& a, const SmallArgs& sa, hipEvent_t ev0,
                     hipEvent_t ev1) {
-  if (M <= 8)
-    hipExtLaunchKernelGGL((rm_small_kernel<MODE, CAM, 8>), grid, dim3(kBlock), 0, st, ev0, ev1, 0u, a, sa);
-  else if (M <= 16)
-    hipExtLaunchKernelGGL((rm_small_kernel<MODE, CAM, 16>), grid, dim3(kBlock), 0, st, ev0, ev1, 0u, a, sa);
-  else
-    hipExtLaunchKernelGGL((rm_small_kernel<MODE, CAM, 32>), grid, dim3(kBlock), 0, st, ev0, ev1, 0u, a, sa);
+  const dim3 blk(kBlock);
+  switch ((M + 3) / 4) {
+    case 1: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 4>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    case 2: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 8>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    case 3: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 12>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    case 4: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 16>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    case 5: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 20>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    case 6: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 24>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    case 7: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 28>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    default: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 32>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+  }
 }
 
 int run_small(rm_context* ctx, const Call& c, KArgs& a, long long n) {
@@ -2996,16 +3002,9 @@ int run_small(rm_context* ctx, const Call& c, KArgs& a, long long n) {
     hipEvent_t ev0, ev1;
     if ((rc = next_events(ctx, ev0, ev1)) != RM_OK) return rc;
     const dim3 grid((unsigned)nb);
-    if (c.mode == kFwd) {
-      if (c.cam) launch_small_m<kFwd, true>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
-      else launch_small_m<kFwd, false>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
-    } else if (c.mode == kBwd) {
-      if (c.cam) launch_small_m<kBwd, true>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
-      else launch_small_m<kBwd, false>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
-    } else {
-      if (c.cam) launch_small_m<kTrain, true>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
-      else launch_small_m<kTrain, false>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
-    }
+    if (c.mode == kFwd) launch_small_m<kFwd>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
+    else if (c.mode == kBwd) launch_small_m<kBwd>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
+    else launch_small_m<kTrain>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
     RM_HIP(ctx, hipGetLastError());
     if (has_bwd && !sa.final_in_kernel && (rc = reduce_and_finalize(ctx, c, a, nb, first)) != RM_OK) return rc;
     done += nr;

@@ -9,13 +9,14 @@
 // finalize). This kernel is written for that regime, M <= kSmallMaxM:
 //  * one launch per call: every block builds the sphere data it needs from the activated
 //    parameters itself (LDS, then registers), and the last block to finish sums the blocks'
-//    partial records in block order and writes the gradients (a release / acquire hand-off on an
-//    arrival counter; launches of more than kSmallFinalMaxBlocks blocks write partial records for
-//    rm_reduce_partials / rm_finalize_grads instead);
-//  * the sphere data of the march live in VGPRs (uniform values: a small launch has one wave per
-//    SIMD, registers are free), the sphere loop runs over the real spheres in groups of four (a
-//    group past M is skipped by a scalar branch; the 1-3 padding spheres of the last group sit at
-//    x = 1e15 and contribute exact zeros, as in rm_prep_kernel);
+//    partial records and writes the gradients (write-through record stores, an arrival counter,
+//    an agent-scope acquire in the last block; launches of more than kSmallFinalMaxBlocks blocks
+//    write partial records for rm_reduce_partials / rm_finalize_grads instead);
+//  * the sphere data of the march live in VGPRs as pairs (uniform values: a small launch has one
+//    wave per SIMD, registers are free), every sweep handles two spheres per packed instruction
+//    over the MB spheres of the kernel's bucket (M rounded up to a multiple of 4: straight-line
+//    code the scheduler interleaves; the 0-3 padding spheres sit at x = 1e15 and contribute exact
+//    zeros, as in rm_prep_kernel);
 //  * every soft-min takes the reference's exact maximum shift (sdf.rs:36-40) per ray: two passes
 //    over the spheres held in registers, no wave-uniform path choice, no matrix-core exchange;
 //  * the backward keeps one ray per lane and sums each sphere's seven gradient terms over the
@@ -23,9 +24,8 @@
 // Deterministic: every sum has a fixed order (lanes, waves, blocks).
 #pragma once
 
-constexpr int kSmallMaxM = 32;           // spheres handled by the small kernel
-constexpr int kSmallGroup = 4;           // sphere loop granularity (scalar-branch groups)
-constexpr int kSmallFinalMaxBlocks = 256;  // in-kernel final reduction up to this many blocks
+constexpr int kSmallMaxM = 32;             // spheres handled by the small kernel
+constexpr int kSmallFinalMaxBlocks = 128;  // in-kernel final reduction up to this many blocks
 
 struct SmallArgs {
   FinalArgs fin;          // where the last block writes the gradients and the loss
@@ -33,51 +33,44 @@ struct SmallArgs {
   int final_in_kernel;    // 1: the last block reduces and finalizes; 0: partial records only
 };
 
-// Per-sphere march data in registers: gx = -2c, cc = |c|^2 (expansion form, scene.rs:66-71),
-// kr = kappa r (kappa = smooth_k log2 e).
+// Per-sphere march data in registers, pair p = spheres (2p, 2p + 1): gx = -2c, cc = |c|^2
+// (expansion form, scene.rs:66-71), kr = kappa r (kappa = smooth_k log2 e).
 template <int MB>
 struct SmallSpheres {
-  float gx[MB], gy[MB], gz[MB], cc[MB], kr[MB];
+  f2 gx[MB / 2], gy[MB / 2], gz[MB / 2], cc[MB / 2], kr[MB / 2];
 };
 
 // Soft-min scene SDF at p (scene.rs:60-79 + sdf.rs:30-44) in base 2 with the exact per-ray max
 // shift: D = -(log2(sum_j 2^(v_j - m)) + m) / kappa, v_j = kappa (r_j - rho_j). RSQ: rho = q rsq(q)
 // (the reconnect: backward sweep 2 recomputes the same v_j bit for bit); else rho = sqrt(q).
 template <int MB, bool RSQ>
-__device__ __forceinline__ float small_softmin(const float p[3], const SmallSpheres<MB>& S, int M, float kappa,
+__device__ __forceinline__ float small_softmin(const float p[3], const SmallSpheres<MB>& S, float kappa,
                                                float inv_kappa, float& m_out, float& s_out) {
-  const float pp = psq(p);
-  float v[MB];
+  const f2 PX = sp(p[0]), PY = sp(p[1]), PZ = sp(p[2]), PP = sp(psq(p)), NK = sp(-kappa);
+  f2 v[MB / 2];
   float m = -INFINITY;
 #pragma unroll
-  for (int j0 = 0; j0 < MB; j0 += kSmallGroup) {
-    if (j0 < M) {
-#pragma unroll
-      for (int j = j0; j < j0 + kSmallGroup; ++j) {
-        const float q = qclamp(fmaf(p[2], S.gz[j], fmaf(p[1], S.gy[j], fmaf(p[0], S.gx[j], pp + S.cc[j]))), 1e-6f);
-        const float rho = RSQ ? q * frsq(q) : fsqrt(q);
-        v[j] = fmaf(-kappa, rho, S.kr[j]);
-        m = fmaxf(m, v[j]);
-      }
-    }
+  for (int i = 0; i < MB / 2; ++i) {
+    f2 q = clamp_q(fma2(PZ, S.gz[i], fma2(PY, S.gy[i], fma2(PX, S.gx[i], PP + S.cc[i]))));
+    const f2 rho = RSQ ? q * rsq2(q) : sqrt2(q);
+    v[i] = fma2(rho, NK, S.kr[i]);
+    m = fmaxf(m, fmaxf(v[i].x, v[i].y));
   }
-  float s = 0.0f;
+  const f2 MN = sp(m);
+  f2 acc = sp(0.0f);
 #pragma unroll
-  for (int j0 = 0; j0 < MB; j0 += kSmallGroup) {
-    if (j0 < M) {
-#pragma unroll
-      for (int j = j0; j < j0 + kSmallGroup; ++j) s += fexp2(v[j] - m);
-    }
-  }
+  for (int i = 0; i < MB / 2; ++i) acc += exp2v(v[i] - MN);
+  const float s = acc.x + acc.y;
   m_out = m;
   s_out = s;
   return -(flog2(fmaxf(s, 1e-8f)) + m) * inv_kappa;
 }
 
-template <int MODE, bool CAM, int MB>
+template <int MODE, int MB>
 __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, const SmallArgs sa) {
-  static_assert(MB % kSmallGroup == 0 && MB <= kSmallMaxM, "sphere bucket");
+  static_assert(MB % 2 == 0 && MB <= kSmallMaxM, "sphere bucket");
   constexpr int kRec = kSmallMaxM * 8 + 8;  // per-wave slot of the cross-wave sums
+  constexpr int NP = MB / 2;
   __shared__ float4 s_geo[MB];              // {gx, gy, gz, cc}
   __shared__ float4 s_mat[MB];              // {kr, r, 0, 0}
   __shared__ float4 s_col[MB];              // {red, green, blue, 0}
@@ -112,17 +105,18 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
   long long ri = a.ray_begin + (valid ? li : 0);
   float o[3], d[3];
   int view;
-  setup_ray<CAM>(a, ri, o, d, view);
+  if (a.num_views > 0) setup_ray<true>(a, ri, o, d, view);
+  else setup_ray<false>(a, ri, o, d, view);
   __syncthreads();
   SmallSpheres<MB> S;
 #pragma unroll
-  for (int j = 0; j < MB; ++j) {
-    const float4 g = s_geo[j];
-    S.gx[j] = g.x;
-    S.gy[j] = g.y;
-    S.gz[j] = g.z;
-    S.cc[j] = g.w;
-    S.kr[j] = s_mat[j].x;
+  for (int i = 0; i < NP; ++i) {
+    const float4 g0 = s_geo[2 * i], g1 = s_geo[2 * i + 1];
+    S.gx[i] = f2{g0.x, g1.x};
+    S.gy[i] = f2{g0.y, g1.y};
+    S.gz[i] = f2{g0.z, g1.z};
+    S.cc[i] = f2{g0.w, g1.w};
+    S.kr[i] = f2{s_mat[2 * i].x, s_mat[2 * i + 1].x};
   }
 
   // ---- march: t <- (t + sdf(o + d t)).detach(), S times (renderer_diff.rs:20-26)
@@ -133,7 +127,7 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
     for (int st = 0; st < a.steps; ++st) {
       const float p[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
       float m, s;
-      t = fminf(t + small_softmin<MB, false>(p, S, M, kappa, inv_kappa, m, s), kTMax);
+      t = fminf(t + small_softmin<MB, false>(p, S, kappa, inv_kappa, m, s), kTMax);
     }
   }
   if (MODE == kFwd && a.t_out != nullptr && valid) a.t_out[ri] = t;
@@ -141,7 +135,7 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
   // ---- reconnect: t_final = t + sdf(p_approx) (renderer_diff.rs:30-39)
   const float pa[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
   float mA, sA;
-  const float Da = small_softmin<MB, true>(pa, S, M, kappa, inv_kappa, mA, sA);
+  const float Da = small_softmin<MB, true>(pa, S, kappa, inv_kappa, mA, sA);
   const float tf = t + Da;
   const float p[3] = {fmaf(d[0], tf, o[0]), fmaf(d[1], tf, o[1]), fmaf(d[2], tf, o[2])};
 
@@ -150,47 +144,39 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
   // limit of scene.rs:81-128 (2 eps grad D, grad D = sum beta_j (p - c_j) / rho_j), two passes:
   // the exact minimum delta, then the sums relative to it (exponents <= 0 exactly)
   const float c10l = a.csharp * kLog2e;
-  const float pp = psq(p);
-  float dl[MB], ir[MB];
+  const f2 PX = sp(p[0]), PY = sp(p[1]), PZ = sp(p[2]), PP = sp(psq(p)), HALF = sp(0.5f);
+  f2 dl[NP], ir[NP];
   float dmin = INFINITY;
 #pragma unroll
-  for (int j0 = 0; j0 < MB; j0 += kSmallGroup) {
-    if (j0 < M) {
-#pragma unroll
-      for (int j = j0; j < j0 + kSmallGroup; ++j) {
-        const float4 mt = s_mat[j];
-        const float q = fmaf(p[2], S.gz[j], fmaf(p[1], S.gy[j], fmaf(p[0], S.gx[j], pp + S.cc[j])));
-        const float qc = qclamp(q, 1e-6f);
-        const float r = frsq(qc);
-        dl[j] = qc * r - mt.y;  // delta_j = rho_j - r_j
-        ir[j] = q >= 1e-6f ? r : 0.0f;  // clamp_min(1e-6) gate: that distance carries no gradient
-        dmin = fminf(dmin, dl[j]);
-      }
-    }
+  for (int i = 0; i < NP; ++i) {
+    const f2 q = fma2(PZ, S.gz[i], fma2(PY, S.gy[i], fma2(PX, S.gx[i], PP + S.cc[i])));
+    const f2 qc = clamp_q(q);
+    const f2 r = rsq2(qc);
+    dl[i] = qc * r - f2{s_mat[2 * i].y, s_mat[2 * i + 1].y};  // delta_j = rho_j - r_j
+    // clamp_min(1e-6) gate: a clamped distance is constant and carries no gradient
+    ir[i] = f2{q.x >= 1e-6f ? r.x : 0.0f, q.y >= 1e-6f ? r.y : 0.0f};
+    dmin = fminf(dmin, fminf(dl[i].x, dl[i].y));
   }
-  float Zw = 0.0f, Zb = 0.0f, C[3] = {0.0f, 0.0f, 0.0f}, G[3] = {0.0f, 0.0f, 0.0f};
+  const f2 DM = sp(dmin), CL = sp(c10l), KA = sp(kappa);
+  f2 Zw2 = sp(0.0f), Zb2 = sp(0.0f), C2[3] = {sp(0.0f), sp(0.0f), sp(0.0f)}, G2[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
 #pragma unroll
-  for (int j0 = 0; j0 < MB; j0 += kSmallGroup) {
-    if (j0 < M) {
-#pragma unroll
-      for (int j = j0; j < j0 + kSmallGroup; ++j) {
-        const float dd = dmin - dl[j];
-        const float ew = fexp2(dd * c10l), eb = fexp2(dd * kappa);
-        const float4 col = s_col[j];
-        Zw += ew;
-        C[0] = fmaf(ew, col.x, C[0]);
-        C[1] = fmaf(ew, col.y, C[1]);
-        C[2] = fmaf(ew, col.z, C[2]);
-        Zb += eb;
-        const float wr = eb * ir[j];
-        G[0] = fmaf(wr, fmaf(0.5f, S.gx[j], p[0]), G[0]);
-        G[1] = fmaf(wr, fmaf(0.5f, S.gy[j], p[1]), G[1]);
-        G[2] = fmaf(wr, fmaf(0.5f, S.gz[j], p[2]), G[2]);
-      }
-    }
+  for (int i = 0; i < NP; ++i) {
+    const f2 dd = DM - dl[i];
+    const f2 ew = exp2v(dd * CL), eb = exp2v(dd * KA);
+    const float4 c0 = s_col[2 * i], c1 = s_col[2 * i + 1];
+    Zw2 += ew;
+    C2[0] = fma2(ew, f2{c0.x, c1.x}, C2[0]);
+    C2[1] = fma2(ew, f2{c0.y, c1.y}, C2[1]);
+    C2[2] = fma2(ew, f2{c0.z, c1.z}, C2[2]);
+    Zb2 += eb;
+    const f2 wr = eb * ir[i];
+    G2[0] = fma2(wr, fma2(HALF, S.gx[i], PX), G2[0]);
+    G2[1] = fma2(wr, fma2(HALF, S.gy[i], PY), G2[1]);
+    G2[2] = fma2(wr, fma2(HALF, S.gz[i], PZ), G2[2]);
   }
+  const float Zw = Zw2.x + Zw2.y, Zb = Zb2.x + Zb2.y;
   const float te = 2.0f * a.eps * frcp(Zb);
-  const float nx = te * G[0], ny = te * G[1], nz = te * G[2];
+  const float nx = te * (G2[0].x + G2[0].y), ny = te * (G2[1].x + G2[1].y), nz = te * (G2[2].x + G2[2].y);
   const float inv_len = frsq(fmaf(nz, nz, fmaf(ny, ny, fmaf(nx, nx, 1e-6f))));
   const float nrm[3] = {nx * inv_len, ny * inv_len, nz * inv_len};
   // ---- lighting (renderer_diff.rs:48-62)
@@ -203,7 +189,7 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
   const float Lgt = fmaf(dif, 1.0f - amb, amb);
   const float Df = dmin - flog2(fmaxf(Zb, 1e-8f)) * inv_kappa;
   const float invZw = frcp(Zw);
-  const float mix[3] = {C[0] * invZw, C[1] * invZw, C[2] * invZw};
+  const float mix[3] = {(C2[0].x + C2[0].y) * invZw, (C2[1].x + C2[1].y) * invZw, (C2[2].x + C2[2].y) * invZw};
   const float mu = frcp(1.0f + fexp2(a.msharp * kLog2e * Df));  // sigmoid(-msharp D)
   const float scale = Lgt * mu;
   const float outv[3] = {mix[0] * scale, mix[1] * scale, mix[2] * scale};
@@ -252,60 +238,63 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
   }
 
   // ---- backward sweep 1 at p_final: g_delta_j (colour softmax + mask soft-min), g_p -> g_t
-  float gdj[MB], wj[MB];
-  float gp[3] = {0.0f, 0.0f, 0.0f};
+  f2 gdj[NP], wj[NP];
+  f2 gp2[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
+  const f2 G0 = sp(gm[0]), G1 = sp(gm[1]), G2c = sp(gm[2]), MG = sp(mg), NCS = sp(-a.csharp), IZ = sp(invZw),
+           BS = sp(b_scale);
 #pragma unroll
-  for (int j0 = 0; j0 < MB; j0 += kSmallGroup) {
-    if (j0 < M) {
-#pragma unroll
-      for (int j = j0; j < j0 + kSmallGroup; ++j) {
-        const float dd = dmin - dl[j];  // <= 0 exactly
-        const float w = fexp2(dd * c10l) * invZw;
-        const float bt = fexp2(dd * kappa) * b_scale;
-        const float4 col = s_col[j];
-        const float cgm = fmaf(col.z, gm[2], fmaf(col.y, gm[1], col.x * gm[0]));
-        const float gd = fmaf(w * -a.csharp, cgm - mg, bt);
-        const float gu = gd * ir[j];
-        gp[0] = fmaf(gu, fmaf(0.5f, S.gx[j], p[0]), gp[0]);
-        gp[1] = fmaf(gu, fmaf(0.5f, S.gy[j], p[1]), gp[1]);
-        gp[2] = fmaf(gu, fmaf(0.5f, S.gz[j], p[2]), gp[2]);
-        gdj[j] = gd;
-        wj[j] = w;
-      }
-    }
+  for (int i = 0; i < NP; ++i) {
+    const f2 dd = DM - dl[i];  // <= 0 exactly
+    const f2 w = exp2v(dd * CL) * IZ;
+    const f2 bt = exp2v(dd * KA) * BS;
+    const float4 c0 = s_col[2 * i], c1 = s_col[2 * i + 1];
+    const f2 cgm = fma2(f2{c0.z, c1.z}, G2c, fma2(f2{c0.y, c1.y}, G1, f2{c0.x, c1.x} * G0));
+    const f2 gd = fma2(w * NCS, cgm - MG, bt);
+    const f2 gu = gd * ir[i];
+    gp2[0] = fma2(gu, fma2(HALF, S.gx[i], PX), gp2[0]);
+    gp2[1] = fma2(gu, fma2(HALF, S.gy[i], PY), gp2[1]);
+    gp2[2] = fma2(gu, fma2(HALF, S.gz[i], PZ), gp2[2]);
+    gdj[i] = gd;
+    wj[i] = w;
   }
+  const float gp[3] = {gp2[0].x + gp2[0].y, gp2[1].x + gp2[1].y, gp2[2].x + gp2[2].y};
   const float gt = fmaf(gp[2], d[2], fmaf(gp[1], d[1], gp[0] * d[0]));  // t_final = t + D(p_a)
-  const float hs = gt * frcp(sA);
   // ---- sweep 2 at p_approx (alpha = softmax(-k dist_a)) and the per-sphere wave sums
-  const float ppa = psq(pa);
+  const f2 AX = sp(pa[0]), AY = sp(pa[1]), AZ = sp(pa[2]), AP = sp(psq(pa)), NK = sp(-kappa), MA = sp(mA),
+           HS = sp(gt * frcp(sA));
 #pragma unroll
-  for (int j0 = 0; j0 < MB; j0 += kSmallGroup) {
-    if (j0 < M) {
-#pragma unroll
-      for (int j = j0; j < j0 + kSmallGroup; ++j) {
-        const float qa = fmaf(pa[2], S.gz[j], fmaf(pa[1], S.gy[j], fmaf(pa[0], S.gx[j], ppa + S.cc[j])));
-        const float qac = qclamp(qa, 1e-6f);
-        const float ra = frsq(qac);
-        const float h = fexp2(fmaf(-kappa, qac * ra, S.kr[j]) - mA) * hs;  // v - mA <= 0 exactly
-        const float hu = qa >= 1e-6f ? h * ra : 0.0f;
-        const float gu = gdj[j] * ir[j];
-        const float ex = fmaf(0.5f, S.gx[j], p[0]), ey = fmaf(0.5f, S.gy[j], p[1]), ez = fmaf(0.5f, S.gz[j], p[2]);
-        const float ax = fmaf(0.5f, S.gx[j], pa[0]), ay = fmaf(0.5f, S.gy[j], pa[1]), az = fmaf(0.5f, S.gz[j], pa[2]);
-        const float vals[8] = {-fmaf(gu, ex, hu * ax), -fmaf(gu, ey, hu * ay), -fmaf(gu, ez, hu * az), -(gdj[j] + h),
-                               wj[j] * gm[0], wj[j] * gm[1], wj[j] * gm[2], 0.0f};
-        const float rs = wave_reduce8(vals, lane);
-        if ((lane & 7) == 7) red[j * 8 + (lane >> 3)] = rs;
-      }
+  for (int i = 0; i < NP; ++i) {
+    const f2 qa = fma2(AZ, S.gz[i], fma2(AY, S.gy[i], fma2(AX, S.gx[i], AP + S.cc[i])));
+    const f2 qac = clamp_q(qa);
+    const f2 ra = rsq2(qac);
+    const f2 h = exp2v(fma2(qac * ra, NK, S.kr[i]) - MA) * HS;  // v - mA <= 0 exactly
+    const f2 hr = h * ra;
+    const f2 hu = f2{qa.x >= 1e-6f ? hr.x : 0.0f, qa.y >= 1e-6f ? hr.y : 0.0f};
+    const f2 gu = gdj[i] * ir[i];
+    const f2 ex = fma2(HALF, S.gx[i], PX), ey = fma2(HALF, S.gy[i], PY), ez = fma2(HALF, S.gz[i], PZ);
+    const f2 ax = fma2(HALF, S.gx[i], AX), ay = fma2(HALF, S.gy[i], AY), az = fma2(HALF, S.gz[i], AZ);
+    const f2 vc[3] = {-fma2(gu, ex, hu * ax), -fma2(gu, ey, hu * ay), -fma2(gu, ez, hu * az)};
+    const f2 vr = -(gdj[i] + h);
+    const f2 vl[3] = {wj[i] * G0, wj[i] * G1, wj[i] * G2c};
+    const float va[8] = {vc[0].x, vc[1].x, vc[2].x, vr.x, vl[0].x, vl[1].x, vl[2].x, 0.0f};
+    const float vb[8] = {vc[0].y, vc[1].y, vc[2].y, vr.y, vl[0].y, vl[1].y, vl[2].y, 0.0f};
+    const float ra0 = wave_reduce8(va, lane), rb0 = wave_reduce8(vb, lane);
+    if ((lane & 7) == 7) {
+      red[(2 * i) * 8 + (lane >> 3)] = ra0;
+      red[(2 * i + 1) * 8 + (lane >> 3)] = rb0;
     }
   }
   __syncthreads();
 
   // ---- the block's partial record [Mpad][8] | 8 scalars (the rm_reduce_partials layout), the
-  // four waves summed in order; padding spheres and the unused column 7 are 0
+  // four waves summed in order; padding spheres and the unused column 7 are 0. For the in-kernel
+  // final reduction the stores are write-through (sc1) and only the columns it reads are written.
   const int Mpad = a.Mpad;
   const int ncols = Mpad * 8 + 8;
+  const int nneed = M * 8 + 8;  // columns of the real spheres, then the scalars
   float* rec = a.partials + blk * a.rec;
-  for (int e = tid; e < ncols; e += kBlock) {
+  auto col_of = [&](int idx) { return idx < M * 8 ? idx : Mpad * 8 + (idx - M * 8); };
+  auto block_sum = [&](int e) {  // record column e: the four waves in order
     const int src = e < Mpad * 8 ? e : kSmallMaxM * 8 + (e - Mpad * 8);
     const bool zero = e < Mpad * 8 ? ((e >> 3) >= M || (e & 7) == 7) : (e - Mpad * 8) >= 5;
     float v = 0.0f;
@@ -314,20 +303,25 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
 #pragma unroll
       for (int w = 1; w < kWaves; ++w) v += s_red[w * kRec + src];
     }
-    if (e == ncols - 1) v = 1.0f;  // scalar 7: live flag (rm_reduce_partials reads every column)
-    rec[e] = v;
+    return e == ncols - 1 ? 1.0f : v;  // scalar 7: live flag (rm_reduce_partials reads every column)
+  };
+  if (!sa.final_in_kernel) {
+    for (int e = tid; e < ncols; e += kBlock) rec[e] = block_sum(e);
+    return;
   }
-  if (!sa.final_in_kernel) return;
+  for (int idx = tid; idx < nneed; idx += kBlock) {
+    const int e = col_of(idx);
+    __hip_atomic_store(rec + e, block_sum(e), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 
-  // ---- last block: sum the blocks' records in block order and write the gradients
-  // (rm_finalize_grads' layout and light-direction Jacobian). Hand-off: every wave drains its
-  // stores, the block barrier, one lane's agent-scope release fence and arrival; the block whose
-  // arrival is the last acquires and reads (MI355X_MICROARCH.md, inter-workgroup visibility).
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's record stores are done
+  // ---- last block: sum the blocks' records and write the gradients (rm_finalize_grads' layout
+  // and light-direction Jacobian). Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility):
+  // write-through record stores, drained by every storing wave before the block barrier; one
+  // lane's agent-scope arrival; the block whose arrival is the last runs an agent-scope acquire
+  // before its loads.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const unsigned prev = __hip_atomic_fetch_add(sa.arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_last = prev == gridDim.x - 1 ? 1 : 0;
   }
@@ -338,31 +332,45 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  // each needed column is summed by `chains` threads (rows b = k mod chains, in order, eight in
+  // flight), the chains then added in order: a fixed order for every launch of this size
   const int nb = gridDim.x;
-  const FinalArgs& f = sa.fin;
-  for (int e = tid; e < ncols; e += kBlock) {
-    // one addition chain per column in block order, eight rows in flight
+  const int chains = max(1, min(8, kBlock / nneed));
+  for (int w = tid; w < nneed * chains; w += kBlock) {
+    const int idx = w % nneed, ch = w / nneed;
+    const long long e = col_of(idx);
     float acc = 0.0f;
-    for (int b0 = 0; b0 < nb; b0 += 8) {
+    for (int b0 = ch; b0 < nb; b0 += 8 * chains) {
       float v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = a.partials[(long long)min(b0 + u, nb - 1) * a.rec + e];
+      for (int u = 0; u < 8; ++u) {
+        const int b = b0 + u * chains;
+        v[u] = __hip_atomic_load(a.partials + (long long)min(b, nb - 1) * a.rec + e, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      }
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        if (b0 + u < nb) acc += v[u];
+        if (b0 + u * chains < nb) acc += v[u];
     }
-    s_red[e] = acc;
+    s_red[ch * nneed + idx] = acc;
   }
   __syncthreads();
-  for (int e = tid; e < Mpad * 8; e += kBlock) {
-    const int j = e >> 3, comp = e & 7;
-    if (j >= M || comp == 7) continue;
+  const FinalArgs& f = sa.fin;
+  auto total = [&](int idx) {
+    float v = s_red[idx];
+    for (int ch = 1; ch < chains; ++ch) v += s_red[ch * nneed + idx];
+    return v;
+  };
+  for (int idx = tid; idx < M * 8; idx += kBlock) {
+    const int j = idx >> 3, comp = idx & 7;
+    if (comp == 7) continue;
     float* dst = comp < 3 ? (f.gc ? f.gc + 3 * j + comp : nullptr)
                           : (comp == 3 ? (f.gr ? f.gr + j : nullptr) : (f.gcol ? f.gcol + 3 * j + (comp - 4) : nullptr));
-    if (dst) *dst = f.accumulate ? *dst + s_red[e] : s_red[e];
+    const float v = total(idx);
+    if (dst) *dst = f.accumulate ? *dst + v : v;
   }
   if (tid == 0) {
-    const float* sc = s_red + Mpad * 8;
+    const float sc[5] = {total(M * 8), total(M * 8 + 1), total(M * 8 + 2), total(M * 8 + 3), total(M * 8 + 4)};
     if (f.gld) {
       const float l0 = f.light_dir[0], l1 = f.light_dir[1], l2 = f.light_dir[2];
       const float len = sqrtf(l0 * l0 + l1 * l1 + l2 * l2);

@@ -19,6 +19,11 @@ for step in "$@"; do
       timeout -k 10 300 python tools/small_batch_sweep.py > $O/small.json 2> $O/small.err || { tail $O/small.err; exit 1; }
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof_small -o run \
         -- python3 tools/small_batch_sweep.py > $O/prof_small.log 2>&1 || { tail $O/prof_small.log; exit 1; } ;;
+    smallm)
+      for m in 4 7 20 32; do
+        timeout -k 10 300 python tools/small_batch_sweep.py --spheres $m --kernels small > $O/small_m$m.json 2>> $O/small.err \
+          || { tail $O/small.err; exit 1; }
+      done ;;
     bench)
       timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
       cat $O/bench.json ;;
