@@ -375,9 +375,15 @@ def main():
     achieved_tf = (flop_per_ray * rays_per_rank * executed_frac / (kern_step_ms * 1e-3) / 1e12
                    if have_stats else None)
     key = f"{W}x{H}_M{M}_S{S}_V{vpg}" + ("_c16" if args.color_dtype == "f16" else "")
-    traffic, traffic_src = _latest_profile("r*_pmc_traffic.json", key, "train_kernel_bytes_per_launch")
+    # per step (the step's launches together), like `achieved`; per launch where no per-step
+    # summary exists for this workload
+    traffic, traffic_src = _latest_profile("r*_pmc_traffic.json", key, "train_kernel_bytes_per_step")
+    traffic_basis = "per step"
+    if traffic is None:
+        traffic, traffic_src = _latest_profile("r*_pmc_traffic.json", key, "train_kernel_bytes_per_launch")
+        traffic_basis = "per launch"
     pmc, pmc_src = _latest_profile("r*_pmc_sq.json", key, "train_kernel")
-    alg_bytes = rays_per_rank * BYTES_PER_RAY_CAMERA
+    alg_bytes = rays_per_rank * BYTES_PER_RAY_CAMERA  # per step (all of this rank's rays)
     mpad = (M + 31) // 32 * 32
     slab_bytes = (rays_per_rank + 255) // 256 * (mpad * 8 + 8) * 4  # partial-gradient slabs, if all written
     canonical = None
@@ -396,6 +402,7 @@ def main():
         "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 4) if have_stats else None,
         "traffic": traffic,
         "traffic_source": traffic_src,
+        "traffic_basis": traffic_basis,
         "kernel_ms": round(kern_avg_ms, 4),
         "kernel_ms_per_step": round(kern_step_ms, 4),
         "launches_timed": launches,
@@ -406,7 +413,7 @@ def main():
         "achieved_all_rays": round(flop_per_ray * rays_per_rank / (kern_step_ms * 1e-3) / 1e12, 3),
         "canonical": canonical,
         "pmc": None if pmc is None else dict(pmc, source=pmc_src),
-        "hbm": {"algorithmic_bytes_per_launch": alg_bytes,
+        "hbm": {"algorithmic_bytes_per_step": alg_bytes,
                 "bytes_per_ray": BYTES_PER_RAY_CAMERA,
                 "achieved_GBs": round(alg_bytes / (kern_step_ms * 1e-3) / 1e9, 2),
                 "peak_GBs": PEAK_HBM_GBS,

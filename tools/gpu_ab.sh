@@ -1,17 +1,38 @@
-#!/bin/bash
-# GPU tests, then bench.py with the defaults and with each extra environment given as an
-# argument (e.g. RM_VALU_ONLY=1, RM_LIB_PATH=burn_raymarching_amd/lib/var/<name>.so); prints
-# value, kernel ms, roofline frac, executed frac, exited-wave share. Every GPU step has its own
-# time limit; a failing step ends the script.
-mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
-rc=$?
-tail -3 gpurun_out/gpu_tests.log
-[ $rc -le 1 ] || exit $rc
-i=0
-for e in "" "$@"; do
-  i=$((i+1))
-  env $e timeout -k 10 200 python bench.py --cpu-baseline off > gpurun_out/ab_$i.json 2>gpurun_out/ab_$i.err || exit $?
-  python -c "import json,sys; d=json.load(open('gpurun_out/ab_$i.json')); r=d['roofline']; print(sys.argv[1] or 'default', d['value'], r['kernel_ms'], r['frac'], r['executed_frac'], d['early_exit']['exited_frac'])" "$e"
+# Same-box A/B of variants on bench configurations, alternating A B A B over ROUNDS rounds.
+# A variant is "default", an environment assignment list ("RM_SPLIT=0 RM_SMALL=1") or
+# "lib:<name>" (the kernel library burn_raymarching_amd/lib/var/<name>.so, built with
+# tools/build_variant.sh). Configs: m (metric, strong default), m10 (10 views per GPU), c2, c3,
+# c4, c5, c5r1 (C5 on a fixed view), c5s (C5 on a 64x64 view).
+#   CONFIGS="m c5" ROUNDS=2 bash tools/gpu_ab.sh default "RM_X=1" lib:trace
+set -o pipefail
+mkdir -p gpurun_out/ab
+ROUNDS=${ROUNDS:-2}
+CONFIGS=${CONFIGS:-"m c2 c5"}
+for r in $(seq 1 $ROUNDS); do
+  i=0
+  for v in "$@"; do
+    i=$((i + 1))
+    unset RM_LIB_PATH
+    envs=""
+    case $v in
+      default) ;;
+      lib:*) export RM_LIB_PATH=burn_raymarching_amd/lib/var/${v#lib:}.so ;;
+      *) envs=$v ;;
+    esac
+    for c in $CONFIGS; do
+      case $c in
+        m) args="--steps 10" ;;
+        m10) args="--views-per-gpu 10 --steps 20" ;;
+        c2) args="--width 256 --height 256 --spheres 64 --views-per-gpu 10 --steps 20" ;;
+        c3) args="--march-steps 64 --views-per-gpu 10 --steps 10" ;;
+        c4) args="--width 1024 --height 1024 --spheres 1024 --march-steps 64 --views-per-gpu 4 --steps 4 --warmup 2" ;;
+        c5) args="--spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 4 --warmup 2" ;;
+        c5r1) args="--spheres 4096 --march-steps 128 --views-per-gpu 1 --ring 1 --steps 4 --warmup 2" ;;
+        c5s) args="--width 64 --height 64 --spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 4 --warmup 2" ;;
+      esac
+      env $envs timeout -k 10 200 python bench.py --cpu-baseline off $args > gpurun_out/ab/${c}_v${i}_$r.json \
+        2> gpurun_out/ab/${c}_v${i}_$r.err || { tail -5 gpurun_out/ab/${c}_v${i}_$r.err; exit 1; }
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], sys.argv[3], d['value'], d['ms_per_step'], r['kernel_ms_per_step'], r['frac'], r['executed_frac'])" gpurun_out/ab/${c}_v${i}_$r.json $c "$v"
+    done
+  done
 done
-exit $rc

@@ -1,16 +1,44 @@
-# bench.py at the other BASELINE.json configs on one MI355X (per-GPU shares; no CPU baseline):
-#   C2 256x256 / 64 spheres / 32 steps / 10 views      C3 512x512 / 256 / 64 steps / 10 views
+# bench.py at the BASELINE.json configs on one MI355X (no CPU baseline), each as a bench line
+# (replays on: executed and canonical fractions), a rocprofv3 --kernel-trace --stats run of the
+# same arguments (replays off), and -- with PMC=1 -- the FETCH_SIZE / WRITE_SIZE / SQ passes of
+# the same arguments, summarised into profiles/<tag>_pmc_{traffic,sq}.json under the config's
+# bench key (what bench.py quotes as roofline.traffic / roofline.pmc for that workload).
+#   C2 256x256 / 64 spheres / 32 steps / 10 views     C3 512x512 / 256 / 64 steps / 10 views
 #   C4 1024x1024 / 1024 / 64 steps, 4 views (the per-GPU share of 32 views on 8 GPUs)
-#   C5 512x512 / 4096 / 128 steps, 1 view              k = 5 at the metric config
+#   C4s the same 32 views on one GPU (strong-scaling N = 1 leg)
+#   C5 512x512 / 4096 / 128 steps, 1 view (fp32 and fp16 colour)     k5: the metric at k = 5
+#   bash tools/gpu_configs.sh <tag> [names...]
 set -o pipefail
-mkdir -p gpurun_out
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+TAG=${1:-r03}
+shift
+ONLY="$*"
+O=gpurun_out/configs_$TAG
+mkdir -p $O
 run() {
-  name=$1; shift
-  timeout -k 10 300 python bench.py --cpu-baseline off "$@" > gpurun_out/cfg_$name.json 2> gpurun_out/cfg_$name.err || exit $?
-  python3 -c "import json,sys; d=json.load(open('gpurun_out/cfg_$name.json')); r=d['roofline']; print(sys.argv[1], d['value'], d['ms_per_step'], r['kernel_ms_per_step'], r['frac'], r['executed_frac'], d['finite'])" "$name" || exit 1
+  name=$1; key=$2; shift 2
+  if [ -n "$ONLY" ] && [[ " $ONLY " != *" $name "* ]]; then return 0; fi
+  timeout -k 10 300 python bench.py --cpu-baseline off "$@" > $O/$name.json 2> $O/$name.err || return $?
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/$O/prof_$name -o run -- python3 bench.py --cpu-baseline off --aux-steps 0 "$@" > $O/prof_$name.log 2>&1 || return $?
+  if [ -n "$PMC" ]; then
+    local PB="python3 bench.py --cpu-baseline off --aux-steps 0 --steps 3 --warmup 1 $*"
+    timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/$O/pmc_${name}_fetch -o run -- $PB > $O/pmc_$name.log 2>&1 && \
+    timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $R/$O/pmc_${name}_write -o run -- $PB >> $O/pmc_$name.log 2>&1 && \
+    timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_MFMA SQ_WAVES --kernel-trace --output-format csv -d $R/$O/pmc_${name}_sq1 -o run -- $PB >> $O/pmc_$name.log 2>&1 && \
+    timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $R/$O/pmc_${name}_sq2 -o run -- $PB >> $O/pmc_$name.log 2>&1 && \
+    RM_NO_EARLY_EXIT=1 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_MFMA SQ_WAVES --kernel-trace --output-format csv -d $R/$O/pmc_${name}_sq1x -o run -- $PB >> $O/pmc_$name.log 2>&1 && \
+    timeout -k 10 300 python3 bench.py --cpu-baseline off --steps 3 --warmup 1 "$@" > $O/${name}_pmcargs.json && \
+    python3 tools/pmc_summary.py $O/pmc_${name}_fetch $O/pmc_${name}_write profiles/${TAG}_pmc_traffic.json $key 4 && \
+    python3 tools/pmc_sq_summary.py profiles/${TAG}_pmc_sq.json $key $O/pmc_${name}_sq1 $O/pmc_${name}_sq2 $O/pmc_${name}_sq1x $O/${name}_pmcargs.json || return 1
+  fi
+  python3 -c "import json,sys; d=json.load(open('$O/$name.json')); r=d['roofline']; print(sys.argv[1], d['value'], d['ms_per_step'], r['kernel_ms_per_step'], r['frac'], r['executed_frac'], (r['canonical'] or {}).get('frac'), d['finite'])" "$name" || return 1
 }
-run C2 --width 256 --height 256 --spheres 64 --march-steps 32 --steps 20 && \
-run C3 --march-steps 64 --steps 10 && \
-run C4 --width 1024 --height 1024 --spheres 1024 --march-steps 64 --views-per-gpu 4 --steps 5 --warmup 2 && \
-run C5 --spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 5 --warmup 2 && \
-run k5 --smooth-k 5 --steps 10
+run C2 256x256_M64_S32_V10 --width 256 --height 256 --spheres 64 --march-steps 32 --views-per-gpu 10 --steps 20 && \
+run C3 512x512_M256_S64_V10 --march-steps 64 --views-per-gpu 10 --steps 20 && \
+run C4 1024x1024_M1024_S64_V4 --width 1024 --height 1024 --spheres 1024 --march-steps 64 --views-per-gpu 4 --steps 6 --warmup 2 && \
+run C4s 1024x1024_M1024_S64_V32 --width 1024 --height 1024 --spheres 1024 --march-steps 64 --global-views 32 --steps 3 --warmup 1 && \
+run C5 512x512_M4096_S128_V1 --spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 6 --warmup 2 && \
+run C5f16 512x512_M4096_S128_V1_c16 --spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 6 --warmup 2 --color-dtype f16 && \
+run k5 512x512_M256_S32_V80 --smooth-k 5 --steps 10 && \
+python3 tools/configs_summary.py $O profiles/${TAG}_configs.json && cp profiles/${TAG}_configs.json $O/

@@ -1,8 +1,11 @@
 # One GPU iteration: the -m gpu suite (stop at the first failure), then optional steps by name.
-#   bash tools/gpu_iter.sh <tag> [tests] [small] [bench] [train]
-# tests: pytest -m gpu; small: tools/small_batch_sweep.py + its rocprofv3 stats; bench: bench.py
-# + rocprofv3 stats; train: the C++ driver's whole schedule (rm_train) timed. Outputs under
-# gpurun_out/<tag>/. Every GPU step runs under its own time limit; the first failure ends the run.
+#   bash tools/gpu_iter.sh <tag> [tests] [small] [smallm] [bench] [train] [trace]
+# tests: pytest -m gpu; small: tools/small_batch_sweep.py + its rocprofv3 stats; smallm: the
+# sweep's small-kernel leg at 4 / 7 / 20 / 32 spheres; bench: bench.py; train: the C++ driver's
+# whole schedule (rm_train) timed + its rocprofv3 stats; trace: per-wave timelines of one train
+# launch (measurement build lib/var/trace.so: bash tools/build_variant.sh WT trace -DRM_BLOCK_TRACE)
+# at the metric, C5, C5 on a 64x64 view and C2. Outputs under gpurun_out/<tag>/. Every GPU step
+# runs under its own time limit; the first failure ends the run.
 set -o pipefail
 export TMPDIR=/tmp
 TAG=${1:-it}
@@ -35,6 +38,15 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof_train -o run \
         -- burn_raymarching_amd/lib/rm_train train --cameras tests/golden/cameras.json --out $O/train_out --no-previews \
         --log-every 0 > $O/prof_train.log 2>&1 || { tail $O/prof_train.log; exit 1; } ;;
+    trace)
+      for c in "metric --bins 20" "c5 --spheres 4096 --march-steps 128 --views 1 --warm 2 --bins 20" \
+               "c5s --width 64 --height 64 --spheres 4096 --march-steps 128 --views 1 --warm 2 --bins 8" \
+               "c2 --width 256 --height 256 --spheres 64 --bins 20"; do
+        set -- $c
+        name=$1; shift
+        RM_LIB_PATH=burn_raymarching_amd/lib/var/trace.so timeout -k 10 200 python tools/block_trace.py \
+          --out $O/bt_$name.npz "$@" > $O/bt_$name.txt 2>&1 || { tail $O/bt_$name.txt; exit 1; }
+      done ;;
   esac
 done
 echo done
