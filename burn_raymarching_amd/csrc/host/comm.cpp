@@ -13,6 +13,9 @@
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -45,7 +48,21 @@ int rccl_broadcast(void* state, float* buf, int64_t count, int32_t root, void* s
   return r == ncclSuccess ? RMH_OK : nccl_fail(r, "ncclBroadcast");
 }
 
-bool read_id(const std::string& path, ncclUniqueId& id) {
+void rccl_abort(void* state) {
+  auto* s = static_cast<Rccl*>(state);
+  if (s && s->comm) {
+    (void)ncclCommAbort(s->comm);  // pending and later collectives of the other ranks fail
+    s->comm = nullptr;
+  }
+}
+
+// The id file, if it was written at or after `since` (seconds since the epoch): a file left by
+// an earlier run is not this run's id.
+bool read_id(const std::string& path, ncclUniqueId& id, double since) {
+  struct stat st;
+  if (stat(path.c_str(), &st) != 0) return false;
+  const double mtime = (double)st.st_mtim.tv_sec + 1e-9 * (double)st.st_mtim.tv_nsec;
+  if (mtime < since) return false;
   FILE* f = std::fopen(path.c_str(), "rb");
   if (!f) return false;
   const size_t n = std::fread(&id, 1, sizeof id, f);
@@ -65,7 +82,10 @@ int rmh_collective_rccl_create(int32_t rank, int32_t world, int32_t device, cons
   if (hipSetDevice(device) != hipSuccess) return fail(RMH_ERR_GPU, "hipSetDevice(%d) failed", device);
   ncclUniqueId id;
   ncclResult_t r;
+  // this rank's start (1 s of slack for file-system timestamp granularity and clock skew)
+  const double since = std::chrono::duration<double>(std::chrono::system_clock::now().time_since_epoch()).count() - 1.0;
   if (rank == 0) {
+    if (world > 1) unlink(id_path);  // an earlier run's id: never this run's
     if ((r = ncclGetUniqueId(&id)) != ncclSuccess) return nccl_fail(r, "ncclGetUniqueId");
     if (world > 1) {
       const std::string tmp = std::string(id_path) + ".tmp";
@@ -76,7 +96,7 @@ int rmh_collective_rccl_create(int32_t rank, int32_t world, int32_t device, cons
     }
   } else {
     const auto t0 = std::chrono::steady_clock::now();
-    while (!read_id(id_path, id)) {
+    while (!read_id(id_path, id, since)) {
       if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > timeout_s)
         return fail(RMH_ERR_IO, "rank %d: no RCCL id at %s after %.0f s", rank, id_path, timeout_s);
       std::this_thread::sleep_for(std::chrono::milliseconds(20));
@@ -87,11 +107,14 @@ int rmh_collective_rccl_create(int32_t rank, int32_t world, int32_t device, cons
     delete s;
     return nccl_fail(r, "ncclCommInitRank");
   }
+  // every rank has joined (ncclCommInitRank is collective): the id file has served its purpose
+  if (rank == 0 && world > 1) unlink(id_path);
   out->state = s;
   out->rank = rank;
   out->world = world;
   out->all_reduce_sum = rccl_all_reduce;
   out->broadcast = rccl_broadcast;
+  out->abort = rccl_abort;
   return RMH_OK;
 }
 

@@ -125,26 +125,40 @@ void rmh_dataset_counts(const rmh_dataset* ds, int64_t* num_fg, int64_t* num_bg)
   if (num_bg) *num_bg = ds ? (int64_t)ds->bg.size() : 0;
 }
 
+void rmh_dataset_sample_count(const rmh_dataset* ds, int32_t batch, float uniform_ratio, int64_t* n_uniform,
+                              int64_t* n_fg) {
+  // dataset.rs:54-61
+  int64_t nu = (int64_t)((float)batch * uniform_ratio);
+  if (nu < 0) nu = 0;
+  if (nu > batch) nu = batch;
+  int64_t nf = batch - nu;
+  const int64_t fg = ds ? (int64_t)ds->fg.size() : 0;
+  if (fg > 0 && fg < nf) {
+    nf = fg;
+    nu = batch - nf;
+  }
+  // dataset.rs:67: with no foreground pixel the boost draws are skipped and the batch is short
+  if (fg == 0) nf = 0;
+  if (n_uniform) *n_uniform = nu;
+  if (n_fg) *n_fg = nf;
+}
+
+void rmh_dataset_fg(const rmh_dataset* ds, const int32_t** fg, int64_t* num_fg) {
+  if (fg) *fg = ds && !ds->fg.empty() ? ds->fg.data() : nullptr;
+  if (num_fg) *num_fg = ds ? (int64_t)ds->fg.size() : 0;
+}
+
 int rmh_dataset_sample(const rmh_dataset* ds, int32_t batch, float uniform_ratio, rmh_rng* rng, int32_t* indices,
                        int32_t* count) {
   if (!ds || !rng || !count || batch < 0 || (batch > 0 && !indices))
     return fail(RMH_ERR_INVALID_ARG, "bad sample args");
   if (ds->num_pixels == 0 && batch > 0) return fail(RMH_ERR_INVALID_ARG, "empty dataset");
-  // dataset.rs:54-61
-  int64_t n_uniform = (int64_t)((float)batch * uniform_ratio);
-  if (n_uniform < 0) n_uniform = 0;
-  if (n_uniform > batch) n_uniform = batch;
-  int64_t n_fg = batch - n_uniform;
+  int64_t n_uniform = 0, n_fg = 0;
+  rmh_dataset_sample_count(ds, batch, uniform_ratio, &n_uniform, &n_fg);
   const int64_t fg = (int64_t)ds->fg.size();
-  if (fg > 0 && fg < n_fg) {
-    n_fg = fg;
-    n_uniform = batch - n_fg;
-  }
   int64_t k = 0;
   for (int64_t i = 0; i < n_uniform; ++i) indices[k++] = (int32_t)rmh_rng_below(rng, (uint32_t)ds->num_pixels);
-  if (fg > 0)
-    for (int64_t i = 0; i < n_fg; ++i) indices[k++] = ds->fg[rmh_rng_below(rng, (uint32_t)fg)];
-  // dataset.rs:67: with no foreground pixel the boost draws are skipped and the batch is short
+  for (int64_t i = 0; i < n_fg; ++i) indices[k++] = ds->fg[rmh_rng_below(rng, (uint32_t)fg)];
   *count = (int32_t)k;
   return RMH_OK;
 }

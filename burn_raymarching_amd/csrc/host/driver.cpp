@@ -46,10 +46,13 @@ struct DevBuf {
   int32_t* i() const { return (int32_t*)p; }
 };
 
-struct PinnedBuf {
-  void* p = nullptr;
-  ~PinnedBuf() {
-    if (p) (void)hipHostFree(p);
+// A rank that leaves rmh_train with an error aborts the collective (rmh_collective.abort), so the
+// other ranks' pending all-reduce / broadcast fail instead of waiting for it forever.
+struct AbortOnError {
+  const rmh_collective* comm = nullptr;
+  bool done = false;
+  ~AbortOnError() {
+    if (!done && comm && comm->world > 1 && comm->abort) comm->abort(comm->state);
   }
 };
 
@@ -163,6 +166,8 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
     return fail(RMH_ERR_INVALID_ARG, "bad collective (rank %d of %d)", rank, world);
   if (cfg->batch < world) return fail(RMH_ERR_INVALID_ARG, "batch %d < %d ranks", cfg->batch, world);
   const bool lead = rank == 0;  // logs, previews and scene.json
+  AbortOnError abort_guard;
+  abort_guard.comm = comm;
   const bool verbose = cfg->log_every > 0 && lead;
 
   // ---- 1. cameras and targets (train.rs:62-96) ----
@@ -198,7 +203,7 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
 
   Gpu g;
   if ((rc = g.open(cfg->device)) != RMH_OK) return rc;
-  DevBuf d_org, d_dir, d_tgt, d_idx, b_org, b_dir, b_tgt;
+  DevBuf d_org, d_dir, d_tgt, d_fg, b_org, b_dir, b_tgt;
   HIPCHK(d_org.alloc(sizeof(float) * 3 * P));
   HIPCHK(d_dir.alloc(sizeof(float) * 3 * P));
   HIPCHK(d_tgt.alloc(sizeof(float) * 3 * P));
@@ -208,28 +213,18 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
   // this rank's share of the batch (B/P rays per rank, the remainder spread)
   auto share = [&](int32_t q) { return cfg->batch / world + (q < cfg->batch % world ? 1 : 0); };
   const int32_t B = share(rank);
-  HIPCHK(d_idx.alloc(sizeof(int32_t) * 2 * (size_t)B));
   HIPCHK(b_org.alloc(sizeof(float) * 3 * (size_t)B));
   HIPCHK(b_dir.alloc(sizeof(float) * 3 * (size_t)B));
   HIPCHK(b_tgt.alloc(sizeof(float) * 3 * (size_t)B));
-  // double-buffered pinned index staging: step s writes half s%2 after that half's copy retired
-  PinnedBuf pin;
-  HIPCHK(hipHostMalloc(&pin.p, sizeof(int32_t) * 2 * (size_t)B, hipHostMallocDefault));
-  hipEvent_t copied[2];
-  HIPCHK(hipEventCreateWithFlags(&copied[0], hipEventDisableTiming));
-  HIPCHK(hipEventCreateWithFlags(&copied[1], hipEventDisableTiming));
-  struct EvGuard {
-    hipEvent_t* e;
-    ~EvGuard() {
-      (void)hipEventDestroy(e[0]);
-      (void)hipEventDestroy(e[1]);
-    }
-  } ev_guard{copied};
-  HIPCHK(hipEventRecord(copied[0], g.stream));
-  HIPCHK(hipEventRecord(copied[1], g.stream));
-
-  rmh_rng rng_sample, rng_split;
-  rmh_rng_seed(&rng_sample, cfg->seed, 1 + 1000 * (uint64_t)rank);  // rank-distinct batches
+  // the foreground list of the dataset, for the device sampler (rm_sample_batch)
+  const int32_t* h_fg = nullptr;
+  int64_t n_fg_list = 0;
+  rmh_dataset_fg(ds.get(), &h_fg, &n_fg_list);
+  HIPCHK(d_fg.alloc(sizeof(int32_t) * (size_t)std::max<int64_t>(n_fg_list, 1)));
+  if (n_fg_list > 0) HIPCHK(hipMemcpyAsync(d_fg.p, h_fg, sizeof(int32_t) * n_fg_list, hipMemcpyHostToDevice, g.stream));
+  // batches: rank-distinct streams of the device sampler, one counter value per step
+  const uint64_t sample_stream = 1 + 1000 * (uint64_t)rank;
+  rmh_rng rng_split;
   rmh_rng_seed(&rng_split, cfg->seed, 2);
 
   // ---- 2. initial model (train.rs:100-126) ----
@@ -277,24 +272,20 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
       const float progress = global_step / total_steps;
       march.smooth_k = 5.0f + (cfg->max_smooth - 5.0f) * progress;  // train.rs:174
       const float uniform_ratio = 0.8f - 0.4f * progress;             // train.rs:176
-      const int half = step & 1;
-      int32_t* hidx = (int32_t*)pin.p + (size_t)half * B;
-      HIPCHK(hipEventSynchronize(copied[half]));
-      int32_t n = 0;
-      if ((rc = rmh_dataset_sample(ds.get(), B, uniform_ratio, &rng_sample, hidx, &n)) != RMH_OK) return rc;
-      // the global ray count of this step (the sampler's count rule per rank: a dataset without
-      // foreground draws only the uniform share, dataset.rs:54-67)
+      // sample_batch (dataset.rs:47-82) on the device: the count rule, then draw + gather
+      int64_t n_uni = 0, n_boost = 0;
+      rmh_dataset_sample_count(ds.get(), B, uniform_ratio, &n_uni, &n_boost);
+      const int64_t n = n_uni + n_boost;
+      // the global ray count of this step: every rank's share under the same count rule
       int64_t n_global = 0;
       for (int32_t q = 0; q < world; ++q) {
-        int64_t nq = share(q);
-        if (nfg == 0) nq = std::min<int64_t>(std::max<int64_t>((int64_t)((float)share(q) * uniform_ratio), 0), nq);
-        n_global += nq;
+        int64_t qu = 0, qf = 0;
+        rmh_dataset_sample_count(ds.get(), share(q), uniform_ratio, &qu, &qf);
+        n_global += qu + qf;
       }
-      int32_t* didx = d_idx.i() + (size_t)half * B;
-      HIPCHK(hipMemcpyAsync(didx, hidx, sizeof(int32_t) * n, hipMemcpyHostToDevice, g.stream));
-      HIPCHK(hipEventRecord(copied[half], g.stream));
-      RMCHK(g.ctx, rm_gather_rays(g.ctx, d_org.f(), d_dir.f(), d_tgt.f(), P, didx, n, b_org.f(), b_dir.f(),
-                                  b_tgt.f()));
+      RMCHK(g.ctx, rm_sample_batch(g.ctx, d_org.f(), d_dir.f(), d_tgt.f(), P, d_fg.i(), n_fg_list, n_uni, n_boost,
+                                   cfg->seed, sample_stream, (uint64_t)global_step, b_org.f(), b_dir.f(), b_tgt.f(),
+                                   nullptr));
       // model.forward + compute_loss + backward (train.rs:182-190), mean over the n*3 elements
       const float inv_count = 1.0f / (3.0f * (float)n_global);
       RMCHK(g.ctx, rm_train_step(g.ctx, b_org.f(), b_dir.f(), b_tgt.f(), n, progress, inv_count, &sc, &march, &gr,
@@ -340,19 +331,23 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
     // rank 0 decides the next generation and broadcasts it: its size, then its raw params
     std::vector<float> next(14 * (size_t)M + 4);
     int32_t nextM = 0;
-    if (lead && (rc = rmh_prune_and_split(raw.data(), M, init_centers.data(), stage, cfg->stages, &rng_split,
-                                          next.data(), &nextM)) != RMH_OK)
-      return rc;
+    int split_rc = RMH_OK;
+    if (lead) split_rc = rmh_prune_and_split(raw.data(), M, init_centers.data(), stage, cfg->stages, &rng_split,
+                                             next.data(), &nextM);
+    if (split_rc != RMH_OK && !comm) return split_rc;
     if (comm) {  // (with one rank too: the RCCL path is the same)
       DevBuf d_next;
       HIPCHK(d_next.alloc(sizeof(float) * next.size()));
-      float fm = (float)nextM;  // M' <= 2M <= 2^17: exact in fp32
+      // the size doubles as the status word: -1 tells every rank that rank 0 failed
+      float fm = split_rc == RMH_OK ? (float)nextM : -1.0f;  // M' <= 2M <= 2^17: exact in fp32
       HIPCHK(hipMemcpyAsync(d_next.p, &fm, sizeof fm, hipMemcpyHostToDevice, g.stream));
       if ((rc = comm->broadcast(comm->state, d_next.f(), 1, 0, g.stream)) != RMH_OK)
         return fail(rc, "broadcast of the next size: %s", rmh_last_error());
       HIPCHK(hipMemcpyAsync(&fm, d_next.p, sizeof fm, hipMemcpyDeviceToHost, g.stream));
       HIPCHK(hipStreamSynchronize(g.stream));
       nextM = (int32_t)fm;
+      if (split_rc != RMH_OK) return split_rc;  // rank 0, after telling the others
+      if (nextM < 0) return fail(RMH_ERR_GPU, "rank 0 failed in prune_and_split (stage %d)", stage);
       if (nextM < 1 || 7 * (size_t)nextM + 4 > next.size()) return fail(RMH_ERR_GPU, "broadcast size %d", nextM);
       const size_t nn = 7 * (size_t)nextM + 4;
       if (lead) HIPCHK(hipMemcpyAsync(d_next.p, next.data(), sizeof(float) * nn, hipMemcpyHostToDevice, g.stream));
@@ -373,6 +368,7 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
                                               7 * M + 4);
     std::memcpy(raw_out, raw.data(), sizeof(float) * (7 * (size_t)M + 4));
   }
+  abort_guard.done = true;
   if (result) {
     result->num_spheres = M;
     result->steps = steps_done;

@@ -117,6 +117,7 @@ int main(int argc, char** argv) {
     rmh_train_config cfg;
     rmh_train_config_default(&cfg);
     int ranks = 0, rank = -1, world = 1;
+    bool device_given = false;
     const char* comm_file = nullptr;
     for (int i = 2; i < argc; ++i) {
       const std::string a = argv[i];
@@ -144,6 +145,7 @@ int main(int argc, char** argv) {
         cfg.log_every = std::atoi(argv[++i]);
       } else if (a == "--device") {
         cfg.device = std::atoi(argv[++i]);
+        device_given = true;
       } else if (a == "--ranks") {
         ranks = std::atoi(argv[++i]);
       } else if (a == "--rank") {
@@ -157,6 +159,12 @@ int main(int argc, char** argv) {
       }
     }
     if (ranks > 0) return launch_ranks(cfg, ranks);
+    // one rank of a run launched elsewhere: without --device it takes LOCAL_RANK's device (or
+    // its rank's): RCCL refuses two ranks on one device
+    if (world > 1 && !device_given) {
+      const char* lr = std::getenv("LOCAL_RANK");
+      cfg.device = lr ? std::atoi(lr) : rank;
+    }
     return train_rank(cfg, rank, world, comm_file);
   }
   if (cmd == "generate") {

@@ -442,7 +442,7 @@ template <bool PAR>
 __device__ void write_origins(const KArgs& a, const float4& S00, const float4& S10, float rmax, float spread,
                               const uint4* At, const float* Wt, float* orig, unsigned char* xch, int v);
 
-__global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __restrict__ rec) {
+__device__ __forceinline__ void prep_body(const KArgs& a0, float4* __restrict__ rec) {
   // One-block case: stage the parameters in LDS once (one load round instead of one per phase:
   // records, MFMA tiles, header, bounding sphere); the phases below read them through `a`.
   __shared__ float stage[7 * kPrepStageMax];
@@ -543,6 +543,8 @@ __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __
 #endif
 }
 
+__global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __restrict__ rec) { prep_body(a0, rec); }
+
 __global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, float* __restrict__ hdr, float* __restrict__ esc,
                                                       int nprep) {
   float rmin = INFINITY, rmax = 0.0f, spread = 0.0f;
@@ -572,6 +574,25 @@ __global__ __launch_bounds__(SPLIT ? 64 * kSplitWaves : 64) void rm_origin_kerne
   const float* Wt = reinterpret_cast<const float*>(At + (size_t)(np / 8) * 64);
   const float* hdr = reinterpret_cast<const float*>(reinterpret_cast<const float2*>(rec + 7 * (size_t)np) + np);
   write_origins<SPLIT>(a, rec[4 * np], rec[5 * np], hdr[1], hdr[2], At, Wt, a.origin, xch, blockIdx.x);
+}
+
+// Small scenes (M <= kPrepOriginMaxM), unsplit launches of up to 16 views: the records and the
+// per-view origin steps in ONE launch of one 1024-thread block -- the records as rm_prep_kernel
+// builds them, then (after the block barrier that makes them visible to the block) wave v
+// computes view v's origin step as rm_origin_kernel would: the same code, the same bits, one
+// dependent launch fewer per call.
+constexpr int kPrepOriginMaxM = 64;
+__global__ __launch_bounds__(1024) void rm_prep_origin_kernel(const KArgs a, float4* __restrict__ rec) {
+  __shared__ __attribute__((aligned(16))) unsigned char xch[16 * kOriginXch];
+  prep_body(a, rec);
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  if (wave >= a.num_views) return;
+  const int np = a.Mpad / 2;
+  const uint4* At = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(rec) + tiles_offset(np, 1));
+  const float* Wt = reinterpret_cast<const float*>(At + (size_t)(np / 8) * 64);
+  const float* hdr = reinterpret_cast<const float*>(reinterpret_cast<const float2*>(rec + 7 * (size_t)np) + np);
+  write_origins<false>(a, rec[4 * np], rec[5 * np], hdr[1], hdr[2], At, Wt, a.origin, xch + wave * kOriginXch, wave);
 }
 
 // ---- packed helpers --------------------------------------------------------------------------
@@ -2371,10 +2392,15 @@ struct FinalArgs {
 #endif
 constexpr int kReduceBatch = RM_REDUCE_BATCH;  // partial rows in flight per thread
 
+__device__ void finalize_block(const float* S, int M, int Mpad, const FinalArgs& f, float* tot);
+
 __global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restrict__ P, long long rec, int M, int Mpad,
-                                                          int nblocks, int seg_len, float* __restrict__ S) {
+                                                          int nblocks, int seg_len, float* __restrict__ S,
+                                                          const FinalArgs f, unsigned* __restrict__ arrivals) {
   __shared__ int rows[256];
   __shared__ int wcount[4];
+  __shared__ float tot[256];
+  __shared__ int last;
   const int ncols = Mpad * 8 + 8;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = blockIdx.x * 256 + tid;
@@ -2404,13 +2430,88 @@ __global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restric
       for (int u = 0; u < kReduceBatch; ++u)
         if (i0 + u < nrows) acc += v1[u];
     }
-    S[(long long)blockIdx.y * ncols + col] = acc;
+    if (arrivals == nullptr) S[(long long)blockIdx.y * ncols + col] = acc;
+    else __hip_atomic_store(S + (long long)blockIdx.y * ncols + col, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (arrivals == nullptr) return;
+  // Pass 2 in the same launch: the segment block that arrives last for this column block sums
+  // the segments and scatters them (finalize_block, the bits of rm_finalize_grads). Hand-off
+  // (MI355X_MICROARCH.md, inter-workgroup visibility): write-through segment stores drained by
+  // every wave before the block barrier, one lane's agent-scope arrival, an agent-scope acquire
+  // and write-through-cache loads in the last block.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(arrivals + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == gridDim.y - 1 ? 1 : 0;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  finalize_block(S, M, Mpad, f, tot);
+  if (tid == 0) __hip_atomic_store(arrivals + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Pass 2 for the 256 columns of pass-1 column block blockIdx.x, by the block of that column block
+// that arrived last: thread t sums column t's kReduceSegs segments in the four chains s mod 4 of
+// rm_finalize_grads, combined (a0 + a1) + (a2 + a3) -- the same bits -- then the scatter.
+__device__ void finalize_block(const float* S, int M, int Mpad, const FinalArgs& f, float* tot) {
+  const int ncols = Mpad * 8 + 8;
+  const int tid = threadIdx.x;
+  const int col = blockIdx.x * 256 + tid;
+  const int c = min(col, ncols - 1);
+  float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int u0 = 0; u0 < kReduceSegs / 4; u0 += 4) {
+    float v[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        v[u][k] = __hip_atomic_load(S + (long long)(4 * (u0 + u) + k) * ncols + c, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) a[k] += v[u][k];
+  }
+  tot[tid] = (a[0] + a[1]) + (a[2] + a[3]);
+  __syncthreads();
+  if (col >= ncols) return;
+  if (col < Mpad * 8) {
+    const int j = col >> 3, comp = col & 7;
+    if (j >= M || comp == 7) return;
+    const float v = tot[tid];
+    float* dst = comp < 3 ? (f.gc ? f.gc + 3 * j + comp : nullptr)
+                          : (comp == 3 ? (f.gr ? f.gr + j : nullptr) : (f.gcol ? f.gcol + 3 * j + (comp - 4) : nullptr));
+    if (dst) *dst = f.accumulate ? *dst + v : v;
+    return;
+  }
+  const int sc = col - Mpad * 8;  // the scalars open their column block (Mpad * 8 % 256 == 0)
+  if (sc == 0 && f.gld) {
+    const float r0 = tot[tid], r1 = tot[tid + 1], r2 = tot[tid + 2];
+    const float l0 = f.light_dir[0], l1 = f.light_dir[1], l2 = f.light_dir[2];
+    const float len = sqrtf(l0 * l0 + l1 * l1 + l2 * l2);
+    const float ln[3] = {l0 / len, l1 / len, l2 / len};
+    const float r[3] = {r0, r1, r2};
+    const float proj = ln[0] * r0 + ln[1] * r1 + ln[2] * r2;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const float gv = (r[k] - ln[k] * proj) / len;
+      f.gld[k] = f.accumulate ? f.gld[k] + gv : gv;
+    }
+  } else if (sc == 3 && f.gamb) {
+    f.gamb[0] = f.accumulate ? f.gamb[0] + tot[tid] : tot[tid];
+  } else if (sc == 4 && f.loss_sum) {
+    f.loss_sum[0] = f.accumulate ? f.loss_sum[0] + tot[tid] : tot[tid];
   }
 }
 
-// Pass 2: sum the segments in order and scatter into the caller's gradient layout (a separate
-// launch: the kernel boundary makes pass 1's sums visible across the XCDs' L2s, which a
-// device-scope fence per block would do at the cost of an L2 writeback each).
+// Pass 2 as its own launch (RM_REDUCE_FUSED=0): sum the segments in order and scatter into the
+// caller's gradient layout.
 // gld = (g_ell - ldn (ldn . g_ell)) / |ld| applies the Jacobian of ld / |ld| (renderer_diff.rs:49-50).
 __global__ __launch_bounds__(256) void rm_finalize_grads(const float* __restrict__ S, int nseg, int M, int Mpad,
                                                          FinalArgs f) {
@@ -2499,6 +2600,38 @@ __global__ __launch_bounds__(256) void rm_gather_kernel(const float* __restrict_
   if (oo) oo[e] = ok ? org[s] : 0.0f;
   if (od) od[e] = ok ? dir[s] : 0.0f;
   if (ot) ot[e] = ok ? tgt[s] : 0.0f;
+}
+
+// SceneDataset::sample_batch on the device (dataset.rs:47-82): batch row i draws its pixel from
+// a counter-based generator -- splitmix64 over key + (i + 1) * golden, the key mixing (seed,
+// stream, counter) -- so a draw depends only on its position, not on the launch geometry: rows
+// i < n_uniform take a pixel uniformly from [0, num_src), the rest a foreground pixel uniformly
+// from fg[0, num_fg) (the index is the high 64 bits of r * n: bias n / 2^64). Then the row's
+// ray origin, direction and target are gathered (dataset.rs:75-79). One thread per row.
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ __launch_bounds__(256) void rm_sample_kernel(const float* __restrict__ org, const float* __restrict__ dir,
+                                                        const float* __restrict__ tgt, long long num_src,
+                                                        const int32_t* __restrict__ fg, long long num_fg,
+                                                        long long n_uniform, long long n, unsigned long long key,
+                                                        float* __restrict__ oo, float* __restrict__ od,
+                                                        float* __restrict__ ot, int32_t* __restrict__ idx_out) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const unsigned long long r = splitmix64(key + (unsigned long long)(i + 1) * 0x9E3779B97F4A7C15ull);
+  long long j;
+  if (i < n_uniform) j = (long long)__umul64hi(r, (unsigned long long)num_src);
+  else j = fg[__umul64hi(r, (unsigned long long)num_fg)];
+  if (idx_out) idx_out[i] = (int32_t)j;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    if (oo) oo[3 * i + c] = org[3 * j + c];
+    if (od) od[3 * i + c] = dir[3 * j + c];
+    if (ot) ot[3 * i + c] = tgt[3 * j + c];
+  }
 }
 
 __global__ __launch_bounds__(256) void rm_activate_kernel(const float* __restrict__ raw, int M,
@@ -2661,6 +2794,49 @@ __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restri
   }
 }
 
+// The optimizer step of a small model (M <= kOptSmallMaxM) in one block: the pre-step parameters
+// into LDS (the snapshot rm_penalty_pairs writes), the repulsion rows of training.rs:73-82 (four
+// threads per sphere, their partials added in order), then optimizer_elem per element and the
+// penalty sum (block tree reduction). One launch instead of three.
+constexpr int kOptSmallMaxM = 64;
+__global__ __launch_bounds__(256) void rm_optimizer_small(float* __restrict__ raw, const float* __restrict__ gact,
+                                                          float* __restrict__ m1, float* __restrict__ m2, int M,
+                                                          int step, float lr, float wd, int with_pen,
+                                                          float* __restrict__ loss_penalty, float* __restrict__ act_out,
+                                                          _Float16* __restrict__ col_h_out) {
+  __shared__ float snap[7 * kOptSmallMaxM + 4];
+  __shared__ float part[4][kOptSmallMaxM][4];
+  __shared__ float pair[kOptSmallMaxM * 4];
+  __shared__ float red[4 * 256];
+  const int tid = threadIdx.x;
+  const int n = 7 * M + 4;
+  for (int i = tid; i < n; i += 256) snap[i] = raw[i];
+  __syncthreads();
+  if (with_pen) {
+    const int s = tid >> 2, k = tid & 3;  // sphere s, columns j = k mod 4
+    if (s < M) {
+      float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      repulsion_row(snap, M, s, k, 4, v);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) part[k][s][c] = v[c];
+    }
+    __syncthreads();
+    if (tid < 4 * M) {
+      const int s2 = tid >> 2, c = tid & 3;
+      pair[4 * s2 + c] = ((part[0][s2][c] + part[1][s2][c]) + part[2][s2][c]) + part[3][s2][c];
+    }
+    __syncthreads();
+  }
+  float pen = 0.0f;
+  for (int i = tid; i < n; i += 256)
+    pen += optimizer_elem(i, snap, raw, gact, m1, m2, pair, M, step, lr, wd, with_pen, act_out, col_h_out);
+  if (loss_penalty != nullptr) {
+    float v[4] = {pen, 0.0f, 0.0f, 0.0f};
+    block_sum4(v, red);
+    if (tid == 0) loss_penalty[0] = v[0];
+  }
+}
+
 __global__ void rm_sum_small(const float* __restrict__ parts, int n, float* __restrict__ out) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     float acc = 0.0f;
@@ -2689,6 +2865,7 @@ struct rm_context {
   int* esc_flags = nullptr;                 // per-block escape flags, kMaxBlocksPerLaunch ints
   void* rec = nullptr;                      // sphere records of the current call (rm_prep_kernel)
   unsigned* arrivals = nullptr;             // rm_small_kernel's arrival counter (zero between launches)
+  unsigned* red_arrivals = nullptr;         // rm_reduce_partials' per-column-block arrival counters
   size_t rec_bytes = 0;
   long long stats_blocks = 0;               // ray blocks launched while stats are on
   long long stats_waves = 0;                // their ray waves (a split block holds one)
@@ -2770,7 +2947,14 @@ int ensure_block_order(rm_context* ctx, int tx, int ty, int sub) {
   return RM_OK;
 }
 
+bool env_is(const char* name, char v) {
+  const char* e = std::getenv(name);
+  return e && e[0] == v;
+}
+
 int pad_spheres(int M) { return (M + kSphereAlign - 1) / kSphereAlign * kSphereAlign; }
+// column blocks of the reduction at the largest scene (RM_MAX_SPHERES): its arrival counters
+constexpr int kRedArrivals = (RM_MAX_SPHERES * 8 + 8 + 255) / 256;
 
 // Ray blocks per per-ray launch: kMaxBlocksPerLaunch, or less with the environment variable
 // RM_MAX_BLOCKS_PER_LAUNCH (tests use it to exercise the sub-launch split at small sizes).
@@ -2914,12 +3098,21 @@ int reduce_and_finalize(rm_context* ctx, const Call& c, const KArgs& a, long lon
   const int segs = kReduceSegs;  // every segment is written (empty ones as 0)
   const int seg_len = (nblocks + segs - 1) / segs;
   const int xblocks = (ncols + 255) / 256;
+  // pass 2 in the same launch (the last-arriving segment block of each column block) unless
+  // RM_REDUCE_FUSED=0 (then rm_finalize_grads: the same bits)
+  const bool fused = !env_is("RM_REDUCE_FUSED", '0');
+  if (fused && !ctx->red_arrivals) {
+    RM_HIP(ctx, hipMalloc(&ctx->red_arrivals, sizeof(unsigned) * kRedArrivals));
+    RM_HIP(ctx, hipMemsetAsync(ctx->red_arrivals, 0, sizeof(unsigned) * kRedArrivals, ctx->stream));
+  }
   hipLaunchKernelGGL(rm_reduce_partials, dim3((unsigned)xblocks, (unsigned)segs), dim3(256), 0, ctx->stream, a.partials,
-                     a.rec, a.M, a.Mpad, nblocks, seg_len, S);
+                     a.rec, a.M, a.Mpad, nblocks, seg_len, S, final_args(c, first), fused ? ctx->red_arrivals : nullptr);
   RM_HIP(ctx, hipGetLastError());
-  hipLaunchKernelGGL(rm_finalize_grads, dim3((unsigned)((ncols + 63) / 64)), dim3(256), 0, ctx->stream, S, segs, a.M,
-                     a.Mpad, final_args(c, first));
-  RM_HIP(ctx, hipGetLastError());
+  if (!fused) {
+    hipLaunchKernelGGL(rm_finalize_grads, dim3((unsigned)((ncols + 63) / 64)), dim3(256), 0, ctx->stream, S, segs, a.M,
+                       a.Mpad, final_args(c, first));
+    RM_HIP(ctx, hipGetLastError());
+  }
   return RM_OK;
 }
 
@@ -2937,11 +3130,6 @@ int next_events(rm_context* ctx, hipEvent_t& ev0, hipEvent_t& ev1) {
   ev1 = ctx->events[ctx->events_used].second;
   ++ctx->events_used;
   return RM_OK;
-}
-
-bool env_is(const char* name, char v) {
-  const char* e = std::getenv(name);
-  return e && e[0] == v;
 }
 
 // Small scenes (M <= kSmallMaxM): rm_small_kernel. Taken by default for ray-array calls (the
@@ -3156,7 +3344,13 @@ int run(rm_context* ctx, const Call& c) {
     a.origin = (c.cam && (c.march->flags & (RM_MARCH_PER_RAY_ORIGIN | RM_MARCH_FORCE_MAX_SHIFT)) == 0)
                    ? reinterpret_cast<float*>((char*)ctx->rec + origin_offset(np, nprep))
                    : nullptr;
-    hipLaunchKernelGGL(rm_prep_kernel, dim3(nprep), dim3(256), 0, ctx->stream, a, (float4*)ctx->rec);
+    // small scenes: records and origin steps in one launch (rm_prep_origin_kernel)
+    const bool fused_origin = a.origin != nullptr && !a.split && nprep == 1 && M <= kPrepOriginMaxM &&
+                              !env_is("RM_PREP_ORIGIN", '0');
+    if (fused_origin)
+      hipLaunchKernelGGL(rm_prep_origin_kernel, dim3(1), dim3(1024), 0, ctx->stream, a, (float4*)ctx->rec);
+    else
+      hipLaunchKernelGGL(rm_prep_kernel, dim3(nprep), dim3(256), 0, ctx->stream, a, (float4*)ctx->rec);
     RM_HIP(ctx, hipGetLastError());
     if (nprep > 1) {
       float* hdr = reinterpret_cast<float*>((char*)ctx->rec + (size_t)np * (7 * 16 + 8));
@@ -3164,7 +3358,7 @@ int run(rm_context* ctx, const Call& c) {
       hipLaunchKernelGGL(rm_prep_finish, dim3(1), dim3(256), 0, ctx->stream, a, hdr, esc, nprep);
       RM_HIP(ctx, hipGetLastError());
     }
-    if (a.origin != nullptr) {
+    if (a.origin != nullptr && !fused_origin) {
       if (a.split)
         hipLaunchKernelGGL(rm_origin_kernel<true>, dim3(c.views), dim3(64 * kSplitWaves), 0, ctx->stream, a,
                            (const float4*)ctx->rec, nprep);
@@ -3462,9 +3656,10 @@ void rm_destroy(rm_context* ctx) {
     if (ctx->ocnt) (void)hipFree(ctx->ocnt);
     if (ctx->rec) (void)hipFree(ctx->rec);
   }
-  if (ctx->arrivals) {
+  if (ctx->arrivals || ctx->red_arrivals) {
     (void)hipStreamSynchronize(ctx->stream);
-    (void)hipFree(ctx->arrivals);
+    if (ctx->arrivals) (void)hipFree(ctx->arrivals);
+    if (ctx->red_arrivals) (void)hipFree(ctx->red_arrivals);
   }
   for (auto& pr : ctx->events) {
     (void)hipEventDestroy(pr.first);
@@ -3689,6 +3884,34 @@ int rm_gather_rays(rm_context* ctx, const float* ray_org, const float* ray_dir, 
   return RM_OK;
 }
 
+int rm_sample_batch(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets, int64_t num_src,
+                    const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform, int64_t n_fg, uint64_t seed,
+                    uint64_t stream, uint64_t counter, float* out_org, float* out_dir, float* out_targets,
+                    int32_t* indices_out) {
+  if (!ctx) return RM_ERR_INVALID_ARG;
+  if (num_src < 0 || num_fg < 0 || n_uniform < 0 || n_fg < 0) return fail(ctx, RM_ERR_INVALID_ARG, "negative size");
+  const long long n = n_uniform + n_fg;
+  if (n == 0) return RM_OK;
+  if (num_src == 0 || num_src > INT32_MAX) return fail(ctx, RM_ERR_INVALID_ARG, "num_src %lld out of [1, 2^31)", (long long)num_src);
+  if (n_fg > 0 && (num_fg == 0 || !fg_indices)) return fail(ctx, RM_ERR_INVALID_ARG, "n_fg > 0 needs foreground indices");
+  if ((out_org && !ray_org) || (out_dir && !ray_dir) || (out_targets && !targets))
+    return fail(ctx, RM_ERR_INVALID_ARG, "an output is requested without its source array");
+  if (!out_org && !out_dir && !out_targets && !indices_out) return fail(ctx, RM_ERR_INVALID_ARG, "no output requested");
+  // the call's key: (seed, stream, counter) mixed on the host
+  auto mix = [](unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  };
+  const unsigned long long key = mix(mix(mix(seed) ^ stream) ^ counter);
+  hipLaunchKernelGGL(rm::rm_sample_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, ray_org, ray_dir,
+                     targets, (long long)num_src, fg_indices, (long long)num_fg, (long long)n_uniform, n, key, out_org,
+                     out_dir, out_targets, indices_out);
+  RM_HIP(ctx, hipGetLastError());
+  return RM_OK;
+}
+
 void rm_scene_from_packed(const float* act, int32_t M, rm_scene* s) {
   if (!s) return;
   s->centers = act;
@@ -3719,6 +3942,13 @@ int rm_optimizer_step_f16(rm_context* ctx, float* raw_packed, const float* grad_
   const int M = num_spheres;
   const int n = 7 * M + 4;
   const int nb = (n + 255) / 256;
+  if (M <= rm::kOptSmallMaxM && !env_is("RM_OPT_SMALL", '0')) {  // one block: snapshot, repulsion rows, update
+    hipLaunchKernelGGL(rm::rm_optimizer_small, dim3(1), dim3(256), 0, ctx->stream, raw_packed, grad_act_packed, adam_m,
+                       adam_v, M, step, lr, weight_decay, with_penalties ? 1 : 0, loss_penalty, act_out,
+                       reinterpret_cast<_Float16*>(colors_f16_out));
+    RM_HIP(ctx, hipGetLastError());
+    return RM_OK;
+  }
   // workspace: snapshot of the pre-step params | repulsion rows [M][4] | penalty partials
   const size_t need = ((size_t)n + 4 * (size_t)M + (size_t)nb + 64) * sizeof(float);
   int rc = ensure_ws(ctx, std::max(ctx->ws_bytes, need));

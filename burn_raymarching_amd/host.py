@@ -37,10 +37,14 @@ BROADCAST_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, 
                                 ctypes.c_void_p)
 
 
+ABORT_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+
+
 class RmhCollective(ctypes.Structure):
-    """rmh_collective: sum all-reduce and broadcast of fp32 device buffers on the driver's stream."""
+    """rmh_collective: sum all-reduce and broadcast of fp32 device buffers on the driver's stream,
+    and the (nullable) abort a failing rank calls."""
     _fields_ = [("state", ctypes.c_void_p), ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
-                ("all_reduce_sum", ALL_REDUCE_FN), ("broadcast", BROADCAST_FN)]
+                ("all_reduce_sum", ALL_REDUCE_FN), ("broadcast", BROADCAST_FN), ("abort", ABORT_FN)]
 
 
 class RmhTrainConfig(ctypes.Structure):
@@ -87,6 +91,8 @@ SIGNATURES = {
     "rmh_dataset_destroy": (None, [_P]),
     "rmh_dataset_counts": (None, [_P, ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
     "rmh_dataset_sample": (ctypes.c_int, [_P, _I32, _F, ctypes.POINTER(RmhRng), _P, _PI32]),
+    "rmh_dataset_sample_count": (None, [_P, _I32, _F, ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
+    "rmh_dataset_fg": (None, [_P, ctypes.POINTER(_PI32), ctypes.POINTER(_I64)]),
     "rmh_prune_and_split": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, ctypes.POINTER(RmhRng), _P, _PI32]),
     "rmh_initial_model": (None, [_P]),
     "rmh_collective_rccl_create": (ctypes.c_int, [_I32, _I32, _I32, _S, ctypes.c_double,
@@ -272,6 +278,18 @@ class Dataset:
         lib().rmh_dataset_counts(self.h, ctypes.byref(fg), ctypes.byref(bg))
         return fg.value, bg.value
 
+    def sample_count(self, batch: int, uniform_ratio: float):
+        """(n_uniform, n_fg) of a batch (dataset.rs:54-67), the rule every sampler shares."""
+        nu, nf = _I64(), _I64()
+        lib().rmh_dataset_sample_count(self.h, batch, uniform_ratio, ctypes.byref(nu), ctypes.byref(nf))
+        return nu.value, nf.value
+
+    def foreground(self) -> np.ndarray:
+        """The foreground pixel indices (dataset.rs:26-35), ascending."""
+        ptr, n = _PI32(), _I64()
+        lib().rmh_dataset_fg(self.h, ctypes.byref(ptr), ctypes.byref(n))
+        return np.ctypeslib.as_array(ptr, shape=(n.value,)).copy() if n.value else np.empty(0, np.int32)
+
     def sample(self, batch: int, uniform_ratio: float, rng: Rng) -> np.ndarray:
         idx = np.empty(batch, np.int32)
         n = _I32()
@@ -318,10 +336,11 @@ def train_config(**kw) -> RmhTrainConfig:
     return cfg
 
 
-def collective(rank: int, world: int, all_reduce_sum, broadcast) -> RmhCollective:
+def collective(rank: int, world: int, all_reduce_sum, broadcast, abort=None) -> RmhCollective:
     """An rmh_collective over Python callables all_reduce_sum(dev_ptr, count, stream) and
-    broadcast(dev_ptr, count, root, stream) (each returns None or raises). The struct keeps the
-    callbacks alive; keep it alive while rmh_train runs."""
+    broadcast(dev_ptr, count, root, stream) (each returns None or raises), and abort() (optional:
+    called by a rank that fails after the collectives began). The struct keeps the callbacks
+    alive; keep it alive while rmh_train runs."""
     def ar(_state, buf, count, stream):
         try:
             all_reduce_sum(buf, count, stream)
@@ -336,8 +355,14 @@ def collective(rank: int, world: int, all_reduce_sum, broadcast) -> RmhCollectiv
         except Exception as e:  # noqa: BLE001
             print(f"broadcast failed: {e!r}")
             return 4
-    c = RmhCollective(None, rank, world, ALL_REDUCE_FN(ar), BROADCAST_FN(bc))
-    c._keep = (c.all_reduce_sum, c.broadcast)
+    def ab(_state):
+        try:
+            abort()
+        except Exception as e:  # noqa: BLE001
+            print(f"abort failed: {e!r}")
+    c = RmhCollective(None, rank, world, ALL_REDUCE_FN(ar), BROADCAST_FN(bc),
+                      ABORT_FN(ab) if abort is not None else ABORT_FN())
+    c._keep = (c.all_reduce_sum, c.broadcast, c.abort)
     return c
 
 

@@ -223,6 +223,20 @@ int rm_gather_rays(rm_context* ctx, const float* ray_org, const float* ray_dir, 
                    int64_t num_src, const int32_t* indices, int64_t num_rays, float* out_org, float* out_dir,
                    float* out_targets);
 
+/* ---- batch sampler on the device: SceneDataset::sample_batch, dataset.rs:47-82 ------------- */
+/* Draws n_uniform pixel indices uniformly from [0, num_src), then n_fg more uniformly from the
+ * foreground list fg_indices[0, num_fg) (device int32; dataset.rs:54-73 -- the counts come from
+ * the caller, see rmh_dataset_sample_count), and gathers those rows of ray_org / ray_dir /
+ * targets ([num_src,3] device arrays) into out_* ([n_uniform+n_fg,3]; any NULL to skip it);
+ * indices_out (nullable, int32) receives the drawn indices. The generator is counter-based (row
+ * i of call (seed, stream, counter) is a splitmix64 draw of those four numbers), so a batch is
+ * reproducible and independent of the launch; the reference's draws (rand::rng()) are unseeded,
+ * so batches match it in distribution. One kernel: no host sampling, no host-to-device copy. */
+int rm_sample_batch(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets, int64_t num_src,
+                    const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform, int64_t n_fg, uint64_t seed,
+                    uint64_t stream, uint64_t counter, float* out_org, float* out_dir, float* out_targets,
+                    int32_t* indices_out);
+
 /* ---- diagnostics ------------------------------------------------------------ */
 /* Per-ray forward intermediates dbg [N][24] = {t, t_final, n.x, n.y, n.z, lighting,
  * mix.r, mix.g, mix.b, D_final, mask, n.l, min delta, Zw, Zb, 0, D(+x), D(-x), D(+y),

@@ -99,6 +99,13 @@ void rmh_dataset_counts(const rmh_dataset* ds, int64_t* num_fg, int64_t* num_bg)
  * the number written: like the reference, a dataset without foreground gives a short batch. */
 int rmh_dataset_sample(const rmh_dataset* ds, int32_t batch, float uniform_ratio, rmh_rng* rng, int32_t* indices,
                        int32_t* count);
+/* The count rule of sample_batch alone (dataset.rs:54-67), shared by rmh_dataset_sample, the
+ * device sampler (rm_sample_batch) and the driver's global ray count: *n_uniform uniform draws
+ * and *n_fg foreground draws (0 without foreground: the short batch). */
+void rmh_dataset_sample_count(const rmh_dataset* ds, int32_t batch, float uniform_ratio, int64_t* n_uniform,
+                              int64_t* n_fg);
+/* The foreground pixel list (ascending; valid while ds lives), for uploading to the device. */
+void rmh_dataset_fg(const rmh_dataset* ds, const int32_t** fg, int64_t* num_fg);
 
 /* ---- training.rs:87-238: prune_and_split ---------------------------------------------- */
 /* raw_packed: the model's RAW params [centers 3M | colors 3M | radius M | light 3 | ambient 1];
@@ -122,10 +129,16 @@ typedef struct rmh_collective {
   int32_t world;
   int (*all_reduce_sum)(void* state, float* buf, int64_t count, void* stream);
   int (*broadcast)(void* state, float* buf, int64_t count, int32_t root, void* stream);
+  /* Nullable. Called by a rank that leaves rmh_train with an error after the collectives began:
+   * it must make the other ranks' pending and later collectives fail instead of waiting for this
+   * rank (the RCCL implementation aborts the communicator). */
+  void (*abort)(void* state);
 } rmh_collective;
-/* RCCL communicator of rank `rank` of `world` on HIP device `device`. Rank 0 creates the
- * ncclUniqueId and publishes it at id_path (write + rename); the other ranks wait for the file
- * up to timeout_s seconds. id_path may be NULL when world == 1. */
+/* RCCL communicator of rank `rank` of `world` on HIP device `device`. Rank 0 removes any file at
+ * id_path, creates the ncclUniqueId and publishes it there (write + rename); the other ranks wait
+ * up to timeout_s seconds for a file written after they started (an id file left by an earlier
+ * run is never used); rank 0 removes the file once every rank has joined. id_path may be NULL
+ * when world == 1. */
 int rmh_collective_rccl_create(int32_t rank, int32_t world, int32_t device, const char* id_path, double timeout_s,
                                rmh_collective* out);
 void rmh_collective_rccl_destroy(rmh_collective* c);

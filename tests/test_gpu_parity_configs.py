@@ -280,3 +280,21 @@ def test_stale_order_counts_recover(rm, oracle, monkeypatch):
     assert step() > nblk  # appended on top of stale counts: the next launch takes the static order
     totals = [step() for _ in range(3)]
     assert totals[-1] == nblk and totals[-2] == nblk
+
+
+def test_shared_march_struct_f16_then_f32(rm):
+    """A march struct shared by an fp16-colour scene and an fp32 scene (bench.py reuses one): the
+    caller's struct is never modified, so the fp32 call after the fp16 one reads fp32 colours."""
+    import torch
+    render, model, native = rm
+    sc = model.synthetic_scene(64, 3)
+    cams = model.ring_cameras(4)[:1]
+    march = native.march_params(16, 32.0)
+    s16, s32 = scene_dev(render, sc, color_f16=True), scene_dev(render, sc)
+    tg = torch.zeros((64 * 64, 3), device="cuda")
+    render.train_step_camera(cams, 64, 64, tg, s16, 32.0, 0.5, 16, march=march)
+    assert march.flags & native.RM_MARCH_COLOR_F16 == 0
+    out_a, out_b = torch.empty_like(tg), torch.empty_like(tg)
+    render.train_step_camera(cams, 64, 64, tg, s32, 32.0, 0.5, 16, march=march, out=out_a)
+    render.train_step_camera(cams, 64, 64, tg, s32, 32.0, 0.5, 16, out=out_b)
+    assert torch.equal(out_a, out_b)

@@ -184,6 +184,25 @@ def test_dataset_small_foreground_and_none(H):
     assert empty.sample(10, 0.5, H.Rng(1)).shape == (5,)  # no foreground: the boost part is skipped
 
 
+def test_sample_count_rule_and_foreground_list(H):
+    """The count rule shared by the host sampler, the device sampler and the driver's global ray
+    count (dataset.rs:54-67), and the foreground list the device sampler draws from."""
+    t = _golden_targets(H)
+    ds = H.Dataset(t)
+    fg_mask = (t[:, 0] + t[:, 1] + t[:, 2]) > np.float32(0.05)
+    assert np.array_equal(ds.foreground(), np.flatnonzero(fg_mask).astype(np.int32))
+    for ratio in (0.8, 0.4, 0.0, 1.0):
+        nu, nf = ds.sample_count(16384, ratio)
+        assert nu == int(np.float32(16384) * np.float32(ratio)) and nu + nf == 16384
+        assert ds.sample(16384, ratio, H.Rng(2)).shape == (nu + nf,)
+    tt = np.zeros((100, 3), np.float32)
+    tt[:3] = 1.0
+    small = H.Dataset(tt)
+    assert small.sample_count(100, 0.5) == (97, 3)  # fg (3) < 50: the boost shrinks to |fg|
+    empty = H.Dataset(np.zeros((64, 3), np.float32))
+    assert empty.sample_count(10, 0.5) == (5, 0) and empty.foreground().size == 0
+
+
 def test_sampler_is_seeded(H):
     t = _golden_targets(H)
     ds = H.Dataset(t)
