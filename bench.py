@@ -15,8 +15,8 @@ GPU, 10 per GPU on 8), so the total work per step is fixed as N grows; a rank is
 calls of up to 16 (one launch each), every call slot on its own rm_context so that its
 cost-ordered dispatch comes from the same views' previous step. `--views-per-gpu V` alone selects
 weak scaling (V views per rank per step). value = rays of all ranks * K / max-over-ranks wall time
-of the K timed steps (barrier + synchronize on both sides). `value_median` / `ms_per_step_median` use the median over the K
-steps of the per-step hipEvent time (max over ranks per step).
+of the K timed steps (barrier + synchronize on both sides). `value_median` / `ms_per_step_median` use the median of the per-step
+hipEvent times of every --timing-every-th timed step (max over ranks per step).
 
 `--gpus N` without WORLD_SIZE in the environment launches N rank processes itself (one per
 GPU, before anything touches a GPU) and exits with the first failing rank's status; under
@@ -84,6 +84,11 @@ def parse():
                     help="weak scaling: views per GPU per step (e.g. 10 = the 10-camera ring of BASELINE "
                          "configs[1-2] = 2,621,440 rays in one launch); exclusive with --global-views")
     ap.add_argument("--ring", type=int, default=10, help="cameras on the target ring (at least the views of a step)")
+    ap.add_argument("--views-per-call", type=int, default=0,
+                    help="views per train call (0: as many as one launch takes, up to 16)")
+    ap.add_argument("--streams", type=int, default=1,
+                    help="HIP streams the calls of a step are spread over (>1: the calls run concurrently, each "
+                         "into its own gradient row, summed in call order before the all-reduce)")
     ap.add_argument("--dump-grad", default=None,
                     help="rank 0 saves the all-reduced [gradient | loss] of step 0 here (.npy; rehearsal tests)")
     ap.add_argument("--radius-range", type=float, nargs=2, default=None,
@@ -192,10 +197,10 @@ def main():
             # the measured run must be what it claims: --gpus ranks, each on its own device
             props = torch.cuda.get_device_properties(local)
             me = (socket.gethostname(), str(props.uuid), f"{props.pci_domain_id}:{props.pci_bus_id}:{props.pci_device_id}")
-            every = [None] * world
-            dist.all_gather_object(every, me)
-            if dist.get_world_size() != args.gpus or len(set(every)) != world:
-                print(f"error: rank {rank}: world {dist.get_world_size()} for --gpus {args.gpus}, devices {every}",
+            devices = [None] * world
+            dist.all_gather_object(devices, me)
+            if dist.get_world_size() != args.gpus or len(set(devices)) != world:
+                print(f"error: rank {rank}: world {dist.get_world_size()} for --gpus {args.gpus}, devices {devices}",
                       file=sys.stderr, flush=True)
                 sys.exit(3)
         else:
@@ -217,6 +222,9 @@ def main():
     rays_global = shard.views_total * npix
     # views per train call (one launch of up to 16 views / 4M rays each)
     views_per_call = max(1, min(native.RM_MAX_VIEWS_PER_CALL, MAX_RAYS_PER_CALL // npix))
+    if args.views_per_call > 0:
+        views_per_call = min(views_per_call, args.views_per_call)
+    ncalls = (vpg + views_per_call - 1) // views_per_call
 
     # ---- synthetic scene, targets, optimizer --------------------------------------------
     rr = tuple(args.radius_range) if args.radius_range else (
@@ -237,9 +245,14 @@ def main():
     march = native.march_params(S, K, skip_escaped=args.skip_escaped == "on")
     # one rm_context per call slot of a step (same stream): each keeps the cost-ordered dispatch
     # state of the views it trains every step
-    ctxs = [rmr.context()] + [native.Context(torch.cuda.current_device(), rmr.context().stream)
-                              for _ in range(1, (vpg + views_per_call - 1) // views_per_call)]
+    # one rm_context per call slot of a step: each keeps the cost-ordered dispatch state of the views
+    # it trains every step; with --streams K the slots are spread over K streams
+    nstreams = max(1, min(args.streams, ncalls))
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(1, nstreams)]
+    ctxs = [rmr.context()] + [native.Context(torch.cuda.current_device(), streams[c % nstreams].cuda_stream)
+                              for c in range(1, ncalls)]
     ctx = Contexts(ctxs)
+    slot_buf = torch.zeros((ncalls, rmm.packed_size(M) + 1), device="cuda") if nstreams > 1 else None
     total_steps = args.warmup + args.steps
     progress = {"i": 0}
 
@@ -252,12 +265,31 @@ def main():
         # calls of up to views_per_call views; the later calls add into the gradient and loss
         first = views[0]
         assert views == [(first + j) % ring for j in range(len(views))]
+        main = torch.cuda.current_stream()
+        if slot_buf is not None:
+            start = torch.cuda.Event()
+            start.record(main)
+        nm = rmm.packed_size(M)
         for c, c0 in enumerate(range(0, len(views), views_per_call)):
             part = views[c0:c0 + views_per_call]
             tg = targets2[part[0]:part[0] + len(part)]
-            rmr.train_step_camera([cams[j] for j in part], W, H, tg.view(-1, 3), model.scene(), K,
-                                  progress=min(progress["i"] / total_steps, 1.0), steps=S, inv_count=inv_count,
-                                  grads_packed=grads_out, loss=loss_out, march=march, accumulate=c > 0, ctx=ctxs[c])
+            kw = dict(progress=min(progress["i"] / total_steps, 1.0), steps=S, inv_count=inv_count, march=march,
+                      ctx=ctxs[c])
+            if slot_buf is None:  # one stream: the later calls add into the gradient and loss
+                rmr.train_step_camera([cams[j] for j in part], W, H, tg.view(-1, 3), model.scene(), K,
+                                      grads_packed=grads_out, loss=loss_out, accumulate=c > 0, **kw)
+                continue
+            st = streams[c % nstreams]
+            st.wait_event(start)
+            with torch.cuda.stream(st):
+                rmr.train_step_camera([cams[j] for j in part], W, H, tg.view(-1, 3), model.scene(), K,
+                                      grads_packed=slot_buf[c, :nm], loss=slot_buf[c, nm:], **kw)
+        if slot_buf is not None:
+            for st in streams[1:]:
+                main.wait_stream(st)
+            tot = slot_buf.sum(0)  # the calls' rows in a fixed order
+            grads_out.copy_(tot[:nm])
+            loss_out.copy_(tot[nm:])
 
     dp = ViewShardedStep(shard, npix, rmm.packed_size(M), "cuda", step_fn, optim_fn=lambda g: opt.step(g, args.lr))
     loss = dp.loss
@@ -289,7 +321,10 @@ def main():
     ctx.collect_timing(reset=True)
     # every n-th step when there are enough to sample (short runs: every step)
     every = max(args.timing_every, 1) if args.steps >= 4 * max(args.timing_every, 1) else 1
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    # per-step events on the sampled steps only: an event record is a barrier packet on the stream
+    # (~5 us of GPU idle each), which would inflate short steps (C2) if every step had two
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) if j % every == 0 else None
+          for j in range(args.steps)]
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -299,9 +334,11 @@ def main():
         timed = args.kernel_timing == "on" and j % every == 0
         ctx.timing(timed)
         timed_steps += timed
-        ev[j][0].record()
+        if ev[j] is not None:
+            ev[j][0].record()
         step(i)
-        ev[j][1].record()
+        if ev[j] is not None:
+            ev[j][1].record()
     host_s = time.perf_counter() - t0  # host time to submit the K steps (before the final sync)
     torch.cuda.synchronize()
     if dist is not None:
@@ -309,7 +346,8 @@ def main():
     elapsed = time.perf_counter() - t0
     ctx.timing(False)
     kern_ms, launches = ctx.collect_timing(reset=True)
-    step_ms = torch.tensor([a.elapsed_time(b) for a, b in ev], dtype=torch.float64, device="cuda")
+    step_ms = torch.tensor([e[0].elapsed_time(e[1]) for e in ev if e is not None], dtype=torch.float64,
+                           device="cuda")
 
     # ---- untimed replays of the timed steps: work statistics, then the canonical kernel time.
     # The training state was snapshotted before the timed region; every step is deterministic,
@@ -446,6 +484,7 @@ def main():
                                    + (", fp16 colour / fp32 SDF" if args.color_dtype == "f16" else ""),
                        "width": W, "height": H, "spheres": M, "march_steps": S, "smooth_k": K,
                        "views_per_gpu": vpg, "global_views": shard.views_total, "views_per_call": views_per_call,
+                       "streams": nstreams,
                        "ring": ring, "rays_per_step": rays_global, "radius_range": list(rr),
                        "color_storage": args.color_dtype, "sdf_dtype": "f32",
                        "parallelism": f"views-dp{world}" + ("" if backend == "nccl" else f" ({backend} rehearsal)")},

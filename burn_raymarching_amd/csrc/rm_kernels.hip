@@ -442,7 +442,7 @@ template <bool PAR>
 __device__ void write_origins(const KArgs& a, const float4& S00, const float4& S10, float rmax, float spread,
                               const uint4* At, const float* Wt, float* orig, unsigned char* xch, int v);
 
-__device__ __forceinline__ void prep_body(const KArgs& a0, float4* __restrict__ rec) {
+__global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __restrict__ rec) {
   // One-block case: stage the parameters in LDS once (one load round instead of one per phase:
   // records, MFMA tiles, header, bounding sphere); the phases below read them through `a`.
   __shared__ float stage[7 * kPrepStageMax];
@@ -543,8 +543,6 @@ __device__ __forceinline__ void prep_body(const KArgs& a0, float4* __restrict__ 
 #endif
 }
 
-__global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __restrict__ rec) { prep_body(a0, rec); }
-
 __global__ __launch_bounds__(256) void rm_prep_finish(const KArgs a, float* __restrict__ hdr, float* __restrict__ esc,
                                                       int nprep) {
   float rmin = INFINITY, rmax = 0.0f, spread = 0.0f;
@@ -574,25 +572,6 @@ __global__ __launch_bounds__(SPLIT ? 64 * kSplitWaves : 64) void rm_origin_kerne
   const float* Wt = reinterpret_cast<const float*>(At + (size_t)(np / 8) * 64);
   const float* hdr = reinterpret_cast<const float*>(reinterpret_cast<const float2*>(rec + 7 * (size_t)np) + np);
   write_origins<SPLIT>(a, rec[4 * np], rec[5 * np], hdr[1], hdr[2], At, Wt, a.origin, xch, blockIdx.x);
-}
-
-// Small scenes (M <= kPrepOriginMaxM), unsplit launches of up to 16 views: the records and the
-// per-view origin steps in ONE launch of one 1024-thread block -- the records as rm_prep_kernel
-// builds them, then (after the block barrier that makes them visible to the block) wave v
-// computes view v's origin step as rm_origin_kernel would: the same code, the same bits, one
-// dependent launch fewer per call.
-constexpr int kPrepOriginMaxM = 64;
-__global__ __launch_bounds__(1024) void rm_prep_origin_kernel(const KArgs a, float4* __restrict__ rec) {
-  __shared__ __attribute__((aligned(16))) unsigned char xch[16 * kOriginXch];
-  prep_body(a, rec);
-  __syncthreads();
-  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  if (wave >= a.num_views) return;
-  const int np = a.Mpad / 2;
-  const uint4* At = reinterpret_cast<const uint4*>(reinterpret_cast<const char*>(rec) + tiles_offset(np, 1));
-  const float* Wt = reinterpret_cast<const float*>(At + (size_t)(np / 8) * 64);
-  const float* hdr = reinterpret_cast<const float*>(reinterpret_cast<const float2*>(rec + 7 * (size_t)np) + np);
-  write_origins<false>(a, rec[4 * np], rec[5 * np], hdr[1], hdr[2], At, Wt, a.origin, xch + wave * kOriginXch, wave);
 }
 
 // ---- packed helpers --------------------------------------------------------------------------
@@ -3344,13 +3323,7 @@ int run(rm_context* ctx, const Call& c) {
     a.origin = (c.cam && (c.march->flags & (RM_MARCH_PER_RAY_ORIGIN | RM_MARCH_FORCE_MAX_SHIFT)) == 0)
                    ? reinterpret_cast<float*>((char*)ctx->rec + origin_offset(np, nprep))
                    : nullptr;
-    // small scenes: records and origin steps in one launch (rm_prep_origin_kernel)
-    const bool fused_origin = a.origin != nullptr && !a.split && nprep == 1 && M <= kPrepOriginMaxM &&
-                              !env_is("RM_PREP_ORIGIN", '0');
-    if (fused_origin)
-      hipLaunchKernelGGL(rm_prep_origin_kernel, dim3(1), dim3(1024), 0, ctx->stream, a, (float4*)ctx->rec);
-    else
-      hipLaunchKernelGGL(rm_prep_kernel, dim3(nprep), dim3(256), 0, ctx->stream, a, (float4*)ctx->rec);
+    hipLaunchKernelGGL(rm_prep_kernel, dim3(nprep), dim3(256), 0, ctx->stream, a, (float4*)ctx->rec);
     RM_HIP(ctx, hipGetLastError());
     if (nprep > 1) {
       float* hdr = reinterpret_cast<float*>((char*)ctx->rec + (size_t)np * (7 * 16 + 8));
@@ -3358,7 +3331,7 @@ int run(rm_context* ctx, const Call& c) {
       hipLaunchKernelGGL(rm_prep_finish, dim3(1), dim3(256), 0, ctx->stream, a, hdr, esc, nprep);
       RM_HIP(ctx, hipGetLastError());
     }
-    if (a.origin != nullptr && !fused_origin) {
+    if (a.origin != nullptr) {
       if (a.split)
         hipLaunchKernelGGL(rm_origin_kernel<true>, dim3(c.views), dim3(64 * kSplitWaves), 0, ctx->stream, a,
                            (const float4*)ctx->rec, nprep);

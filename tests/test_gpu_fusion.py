@@ -1,8 +1,6 @@
 """Launch fusions that must not change a bit:
   * the reduction's second pass inside rm_reduce_partials (the last-arriving segment block of each
     column block, RM_REDUCE_FUSED) against its own launch (rm_finalize_grads);
-  * the records and the per-view origin steps of small scenes in one launch
-    (rm_prep_origin_kernel, RM_PREP_ORIGIN) against rm_prep_kernel + rm_origin_kernel;
   * the one-block optimizer of small models (rm_optimizer_small) against the oracle-free
     reference of test_gpu_parity.py (covered there); here: repeated steps are deterministic."""
 import numpy as np
@@ -33,8 +31,7 @@ def _train(torch, model, render, m, views, w, steps):
 
 
 @pytest.mark.parametrize("env,m,views,w", [("RM_REDUCE_FUSED", 64, 3, 128), ("RM_REDUCE_FUSED", 256, 2, 256),
-                                           ("RM_REDUCE_FUSED", 1100, 1, 64), ("RM_PREP_ORIGIN", 64, 10, 64),
-                                           ("RM_PREP_ORIGIN", 40, 16, 32), ("RM_PREP_ORIGIN", 33, 1, 48)])
+                                           ("RM_REDUCE_FUSED", 1100, 1, 64), ("RM_REDUCE_FUSED", 40, 16, 32)])
 def test_fused_launch_is_bitwise_equal(mods, monkeypatch, env, m, views, w):
     torch, model, _, render = mods
     res = {}
