@@ -2443,17 +2443,19 @@ __device__ void finalize_block(const float* S, int M, int Mpad, const FinalArgs&
   const int tid = threadIdx.x;
   const int col = blockIdx.x * 256 + tid;
   const int c = min(col, ncols - 1);
+  // 64 loads in flight per thread (the last block runs alone: registers are free), two rounds
+  constexpr int kU = 16;
   float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (int u0 = 0; u0 < kReduceSegs / 4; u0 += 4) {
-    float v[4][4];
+  for (int u0 = 0; u0 < kReduceSegs / 4; u0 += kU) {
+    float v[kU][4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < kU; ++u)
 #pragma unroll
       for (int k = 0; k < 4; ++k)
         v[u][k] = __hip_atomic_load(S + (long long)(4 * (u0 + u) + k) * ncols + c, __ATOMIC_RELAXED,
                                     __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int u = 0; u < kU; ++u)
 #pragma unroll
       for (int k = 0; k < 4; ++k) a[k] += v[u][k];
   }
@@ -2503,7 +2505,7 @@ __global__ __launch_bounds__(256) void rm_finalize_grads(const float* __restrict
   const int cl = threadIdx.x & 63, chain = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + cl;
   (void)nseg;  // == kReduceSegs always (pass 1 writes every segment, empty ones as 0)
-  static_assert(kReduceSegs % 4 == 0, "four chains");
+  static_assert(kReduceSegs % 64 == 0, "four chains of 16-load rounds");
   {
     float v[kReduceSegs / 4];
     const int c = min(col, ncols - 1);
