@@ -69,6 +69,37 @@ def main():
                 rows.append({"kernel": kern, "rays": n, "march_steps": steps, "us_per_call": round(us, 2),
                              "Mrays_s": round(n / us, 1)})
                 print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
+    # camera mode (rm_train_step_camera): BASELINE configs[0] (64x64, 1 view, 16 steps) and the
+    # preview / driver image size (256x256, 40 steps), one view, both kernels
+    cams = model.ring_cameras(10)[:1]
+    mc = native.cameras(cams)
+    for kern in args.kernels.split(","):
+        os.environ["RM_SMALL"] = "1" if kern == "small" else "0"
+        for size, steps in ((64, 16), (256, 40)):
+            n = size * size
+            tg = torch.rand((n, 3), device="cuda", generator=torch.Generator("cuda").manual_seed(size))
+            march = sc.march_for(native.march_params(steps, args.k))
+            scs = sc.c_struct()
+
+            def call():
+                ctx.check(ctx._lib.rm_train_step_camera(ctx.handle, mc, 1, size, size, ctypes.c_void_p(tg.data_ptr()),
+                                                        0.5, 1.0 / (3 * n), ctypes.byref(scs), ctypes.byref(march),
+                                                        ctypes.byref(cg), ctypes.c_void_p(loss.data_ptr()), None, 0),
+                          "rm_train_step_camera")
+
+            for _ in range(10):
+                call()
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(50):
+                call()
+            e1.record()
+            torch.cuda.synchronize()
+            us = e0.elapsed_time(e1) / 50 * 1e3
+            rows.append({"kernel": kern, "camera": f"{size}x{size}", "rays": n, "march_steps": steps,
+                         "us_per_call": round(us, 2), "Mrays_s": round(n / us, 1)})
+            print(json.dumps(rows[-1]), file=sys.stderr, flush=True)
     print(json.dumps({"spheres": args.spheres, "k": args.k, "rows": rows}))
 
 
