@@ -1,10 +1,11 @@
 # One GPU iteration: the -m gpu suite (stop at the first failure), then optional steps by name.
-#   bash tools/gpu_iter.sh <tag> [tests] [small] [smallm] [bench] [train] [trace]
+#   bash tools/gpu_iter.sh <tag> [tests] [small] [smallm] [bench] [train] [trace] [calib]
 # tests: pytest -m gpu; small: tools/small_batch_sweep.py + its rocprofv3 stats; smallm: the
 # sweep's small-kernel leg at 4 / 7 / 20 / 32 spheres; bench: bench.py; train: the C++ driver's
 # whole schedule (rm_train) timed + its rocprofv3 stats; trace: per-wave timelines of one train
 # launch (measurement build lib/var/trace.so: bash tools/build_variant.sh WT trace -DRM_BLOCK_TRACE)
-# at the metric, C5, C5 on a 64x64 view and C2. Outputs under gpurun_out/<tag>/. Every GPU step
+# at the metric, C5, C5 on a 64x64 view and C2; calib: FETCH_SIZE / WRITE_SIZE of tools/fetch_calib
+# (known byte counts; build it first) into profiles/<tag>_fetch_calibration.json. Outputs under gpurun_out/<tag>/. Every GPU step
 # runs under its own time limit; the first failure ends the run.
 set -o pipefail
 export TMPDIR=/tmp
@@ -38,6 +39,14 @@ for step in "$@"; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof_train -o run \
         -- burn_raymarching_amd/lib/rm_train train --cameras tests/golden/cameras.json --out $O/train_out --no-previews \
         --log-every 0 > $O/prof_train.log 2>&1 || { tail $O/prof_train.log; exit 1; } ;;
+    calib)
+      timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$O/calib_fetch \
+        -o run -- ./tools/fetch_calib > $O/calib_bytes.json 2> $O/calib.log && \
+      timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $GRAFT_REPO_ROOT/$O/calib_write \
+        -o run -- ./tools/fetch_calib > /dev/null 2>> $O/calib.log && \
+      python3 tools/fetch_calib.py $O/calib_fetch $O/calib_write $O/calib_bytes.json profiles/${TAG}_fetch_calibration.json \
+        || { tail $O/calib.log; exit 1; }
+      cp profiles/${TAG}_fetch_calibration.json $O/ ;;
     trace)
       for c in "metric --bins 20" "c5 --spheres 4096 --march-steps 128 --views 1 --warm 2 --bins 20" \
                "c5s --width 64 --height 64 --spheres 4096 --march-steps 128 --views 1 --warm 2 --bins 8" \

@@ -3,7 +3,7 @@
 # two SQ groups; the SQ instruction group again with the early exit off), their summaries into
 # profiles/<tag>_pmc_*.json, then the default bench line (which quotes those summaries) and the
 # rocprofv3 kernel-trace stats of the same command. Outputs under gpurun_out/<tag>/.
-#   bash tools/gpu_round.sh <tag> [extra bench args...]      (SKIP_TESTS=1: measurement only)
+#   bash tools/gpu_round.sh <tag> [extra bench args...]   (SKIP_TESTS=1: measurement only; CALIB=<json>)
 set -o pipefail
 export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT
@@ -34,7 +34,7 @@ pmc sq1 SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_MFMA SQ_WAVES && \
 pmc sq2 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE && \
 pmc_noexit sq1x SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_MFMA SQ_WAVES && \
 timeout -k 10 300 python3 bench.py --steps 5 --warmup 2 --cpu-baseline off $EXTRA > $O/bench_pmcargs.json && \
-python3 tools/pmc_summary.py $O/pmc_fetch $O/pmc_write profiles/${TAG}_pmc_traffic.json $KEY 7 && \
+python3 tools/pmc_summary.py $O/pmc_fetch $O/pmc_write profiles/${TAG}_pmc_traffic.json $KEY 7 $CALIB && \
 python3 tools/pmc_sq_summary.py profiles/${TAG}_pmc_sq.json $KEY $O/pmc_sq1 $O/pmc_sq2 $O/pmc_sq1x $O/bench_pmcargs.json && \
 cp profiles/${TAG}_pmc_traffic.json profiles/${TAG}_pmc_sq.json $O/ && \
 timeout -k 10 300 python bench.py $EXTRA > $O/bench.json 2> $O/bench.err && \

@@ -4,13 +4,14 @@ bench steps the passes ran (warm-up + timed), per step -- a step may hold severa
 strong-scaling default issues 16 views per launch; C5 adds a continuation launch). bench.py
 quotes the per-step figure next to its per-step achieved rate.
 
-    python3 tools/pmc_summary.py FETCH_DIR WRITE_DIR OUT.json KEY [STEPS]
+    python3 tools/pmc_summary.py FETCH_DIR WRITE_DIR OUT.json KEY [STEPS [CALIB.json]]
 
 MI355X_MICROARCH.md §HBM: FETCH_SIZE/WRITE_SIZE are in KiB and come from the L2's fabric-side
 request counters; on gfx950 FETCH_SIZE reads 1/2 of the bytes of wide (16 B/lane) coalesced
-streams. This kernel's global reads are dword-wide (targets, sphere tables, all L2/MALL
-resident) and its stores dword-wide partial slabs, for which the guide has no calibration, so
-both the raw and the x2-corrected read figure are recorded and the raw sum is used.
+streams, and other widths are uncalibrated. This kernel's HBM reads are dword-wide (the AoS
+float3 targets) and its stores dword-wide partial records, so CALIB.json (tools/fetch_calib.py:
+the same widths on known byte counts) supplies the factors: traffic = FETCH x read_f3_factor +
+WRITE x write_dword_factor. Without it the raw sum is recorded.
 """
 import csv
 import glob
@@ -39,6 +40,9 @@ def per_kernel(path, counter):
 def main():
     fetch_dir, write_dir, out, key = sys.argv[1], sys.argv[2], sys.argv[3], sys.argv[4]
     steps = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+    calib = json.load(open(sys.argv[6])) if len(sys.argv) > 6 else None
+    rf = calib["read_f3_factor"] if calib else 1.0
+    wf = calib["write_dword_factor"] if calib else 1.0
     f = per_kernel(fetch_dir, "FETCH_SIZE")
     w = per_kernel(write_dir, "WRITE_SIZE")
     names = [k for k in f if "rm_ray_kernel<2, true" in k]  # camera-mode train kernel (split or not)
@@ -49,14 +53,15 @@ def main():
     fk = sum(fv) / len(fv)
     wk = sum(wv) / max(len(wv), 1)
     data = json.load(open(out)) if os.path.exists(out) else {}
-    data.setdefault("train_kernel_bytes_per_launch", {})[key] = (fk + wk) * 1024.0
+    data.setdefault("train_kernel_bytes_per_launch", {})[key] = (fk * rf + wk * wf) * 1024.0
     if steps > 0:
-        data.setdefault("train_kernel_bytes_per_step", {})[key] = (sum(fv) + sum(wv)) * 1024.0 / steps
+        data.setdefault("train_kernel_bytes_per_step", {})[key] = (sum(fv) * rf + sum(wv) * wf) * 1024.0 / steps
     data.setdefault("detail", {})[key] = {
         "kernels": names, "FETCH_SIZE_KiB_per_launch": fk, "WRITE_SIZE_KiB_per_launch": wk, "launches": len(fv),
-        "steps": steps, "fetch_bytes_x2_corrected_per_launch": fk * 2048.0,
-        "note": "dword-wide accesses: the gfx950 FETCH x2 correction applies to 16 B/lane streams only; raw "
-                "FETCH+WRITE used as traffic"}
+        "steps": steps, "raw_bytes_per_launch": (fk + wk) * 1024.0,
+        "calibration": {"read_f3_factor": rf, "write_dword_factor": wf, "file": sys.argv[6]} if calib else None,
+        "note": "traffic = FETCH x read factor + WRITE x write factor (dword-wide accesses, calibrated on known "
+                "byte counts by tools/fetch_calib)" if calib else "uncalibrated raw FETCH+WRITE"}
     json.dump(data, open(out, "w"), indent=1)
     print(json.dumps(data["detail"][key]))
 
