@@ -1,4 +1,4 @@
-"""Collect the per-config bench lines and rocprofv3 stats of tools/gpu_configs2.sh into one
+"""Collect the per-config bench lines and rocprofv3 stats of tools/gpu_configs.sh into one
 profiles/<tag>_configs.json: per config the bench numbers (value, ms per step, train-kernel time,
 executed and canonical roofline fractions) and, from the rocprofv3 --stats run of the same
 arguments, the average time per call of every kernel and the per-step time outside the train
@@ -22,12 +22,16 @@ def main():
             d = json.load(open(path))
         except ValueError:
             continue
+        if "config" not in d:  # not a bench line (e.g. an earlier summary copied alongside)
+            continue
         r = d.get("roofline") or {}
         entry = {"config": d["config"], "value": d["value"], "value_median": d.get("value_median"),
                  "ms_per_step": d["ms_per_step"], "ms_per_step_median": d.get("ms_per_step_median"),
                  "train_kernel_ms": r.get("kernel_ms_per_step"), "frac": r.get("frac"),
                  "executed_frac": r.get("executed_frac"), "canonical_frac": (r.get("canonical") or {}).get("frac"),
                  "finite": d.get("finite")}
+        if r.get("kernel_ms_per_step") is not None:  # the step's wall time outside the train kernel
+            entry["outside_us_per_step"] = round((d["ms_per_step"] - r["kernel_ms_per_step"]) * 1e3, 2)
         stats = glob.glob(os.path.join(src, f"prof_{name}", "**", "*kernel_stats.csv"), recursive=True)
         if stats:
             rows = list(csv.DictReader(open(stats[0])))
@@ -44,9 +48,11 @@ def main():
                 entry["rocprof_train_avg_us"] = train["avg_us"]
                 entry["rocprof_train_launches_per_step"] = round(train["calls"] / steps, 2)
                 entry["rocprof_train_us_per_step"] = round(train["avg_us"] * train["calls"] / steps, 2)
+                # the per-step kernels besides the train kernel (one-off setup launches, e.g. the
+                # target render, run fewer times than there are steps)
                 other = sum(v["avg_us"] * v["calls"] for k, v in kern.items()
-                            if k.startswith("rm::") or "rm_optimizer" in k or "rm_ray_kernel<2" in k)
-                entry["rocprof_other_us_per_step"] = round((other - train["avg_us"] * train["calls"]) / steps, 2)
+                            if ("rm::" in k or "rm_optimizer" in k) and "rm_ray_kernel" not in k and v["calls"] >= steps)
+                entry["rocprof_other_us_per_step"] = round(other / steps, 2)
         res[name] = entry
     json.dump(res, open(out, "w"), indent=1)
     for k, v in res.items():

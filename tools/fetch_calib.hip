@@ -8,6 +8,9 @@
 //   read_x4      1 GiB, one float4 per lane (the guide's calibrated case: FETCH = bytes / 2)
 //   write_dword  256 MiB, one float per lane per iteration (as the partial records)
 //   write_x4     256 MiB, one float4 per lane
+//   write_rec    256 MiB of 8224-B records in the train kernel's pattern: a block writes its
+//                record's 8 columns per sphere (coalesced dwords), then adds to columns 0-3
+//                (4 of every 8 dwords, read-modify-write) -- counted once as unique bytes
 // Run under `rocprofv3 --pmc FETCH_SIZE` and, separately, `--pmc WRITE_SIZE`; tools/fetch_calib.py
 // turns the per-dispatch counters into bytes-per-counted-byte factors.
 //   hipcc --offload-arch=gfx950 -O3 -o tools/fetch_calib tools/fetch_calib.hip
@@ -60,6 +63,17 @@ __global__ void write_x4(float4* __restrict__ a, long n4) {
   }
 }
 
+constexpr int kRec = 2056;  // floats per record at 256 spheres (8 per sphere + 8 scalars)
+__global__ void write_rec(float* __restrict__ a, long nrec) {
+  for (long b = blockIdx.x; b < nrec; b += gridDim.x) {
+    float* rec = a + b * kRec;
+    for (int e = threadIdx.x; e < kRec; e += blockDim.x) rec[e] = (float)(b + e);
+    __syncthreads();
+    for (int e = threadIdx.x; e < (kRec - 8) / 2; e += blockDim.x) rec[(e >> 2) * 8 + (e & 3)] += 1.0f;
+    __syncthreads();
+  }
+}
+
 int main() {
   const long rbytes = 1L << 30, wbytes = 1L << 28;
   float *r, *w, *sink;
@@ -74,11 +88,13 @@ int main() {
   hipLaunchKernelGGL(read_x4, dim3(grid), dim3(block), 0, 0, (const float4*)r, nr / 4, sink);
   hipLaunchKernelGGL(write_dword, dim3(grid), dim3(block), 0, 0, w, nw);
   hipLaunchKernelGGL(write_x4, dim3(grid), dim3(block), 0, 0, (float4*)w, nw / 4);
+  const long nrec = nw / kRec;
+  hipLaunchKernelGGL(write_rec, dim3(grid), dim3(block), 0, 0, w, nrec);
   CHECK(hipGetLastError());
   CHECK(hipDeviceSynchronize());
   // the exact byte counts each dispatch moves (read_f3 covers 3 * floor(n / 3) floats)
-  std::printf("{\"read_dword\": %ld, \"read_f3\": %ld, \"read_x4\": %ld, \"write_dword\": %ld, \"write_x4\": %ld}\n",
-              rbytes, (nr / 3) * 3 * 4, rbytes, wbytes, wbytes);
+  std::printf("{\"read_dword\": %ld, \"read_f3\": %ld, \"read_x4\": %ld, \"write_dword\": %ld, \"write_x4\": %ld, "
+              "\"write_rec\": %ld}\n", rbytes, (nr / 3) * 3 * 4, rbytes, wbytes, wbytes, nrec * kRec * 4);
   CHECK(hipFree(r));
   CHECK(hipFree(w));
   CHECK(hipFree(sink));

@@ -4,7 +4,8 @@
 
 For each calibration kernel: counted bytes (counter KiB x 1024) and the factor true / counted.
 tools/pmc_summary.py multiplies the train kernel's FETCH_SIZE by the dword-read factor (its reads
-are dword-wide) and its WRITE_SIZE by the dword-write factor.
+are dword-wide) and its WRITE_SIZE by the record-pattern factor (write_rec: the partial records are written, then
+half of their columns read-modified-written).
 """
 import json
 import sys
@@ -27,6 +28,7 @@ def main():
         res[name] = {"bytes": nbytes, "counted_bytes": counted, "factor": nbytes / counted}
     data = {"kernels": res, "read_dword_factor": res["read_dword"]["factor"],
             "read_f3_factor": res["read_f3"]["factor"], "write_dword_factor": res["write_dword"]["factor"],
+            "write_rec_factor": res["write_rec"]["factor"],
             "note": "factor = true bytes / (counter KiB x 1024); tools/fetch_calib.hip, one dispatch each"}
     json.dump(data, open(out, "w"), indent=1)
     print(json.dumps(data))

@@ -29,7 +29,7 @@ run() {
     timeout -k 10 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --kernel-trace --output-format csv -d $R/$O/pmc_${name}_sq2 -o run -- $PB >> $O/pmc_$name.log 2>&1 && \
     RM_NO_EARLY_EXIT=1 timeout -k 10 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_MFMA SQ_WAVES --kernel-trace --output-format csv -d $R/$O/pmc_${name}_sq1x -o run -- $PB >> $O/pmc_$name.log 2>&1 && \
     timeout -k 10 300 python3 bench.py --cpu-baseline off --steps 3 --warmup 1 "$@" > $O/${name}_pmcargs.json && \
-    python3 tools/pmc_summary.py $O/pmc_${name}_fetch $O/pmc_${name}_write profiles/${TAG}_pmc_traffic.json $key 4 $CALIB && \
+    python3 tools/pmc_summary.py $O/pmc_${name}_fetch $O/pmc_${name}_write profiles/${TAG}_pmc_traffic.json $key auto $CALIB && \
     python3 tools/pmc_sq_summary.py profiles/${TAG}_pmc_sq.json $key $O/pmc_${name}_sq1 $O/pmc_${name}_sq2 $O/pmc_${name}_sq1x $O/${name}_pmcargs.json || return 1
   fi
   python3 -c "import json,sys; d=json.load(open('$O/$name.json')); r=d['roofline']; print(sys.argv[1], d['value'], d['ms_per_step'], r['kernel_ms_per_step'], r['frac'], r['executed_frac'], (r['canonical'] or {}).get('frac'), d['finite'])" "$name" || return 1

@@ -34,7 +34,7 @@ pmc sq1 SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_MFMA SQ_WAVES && \
 pmc sq2 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE && \
 pmc_noexit sq1x SQ_INSTS_VALU SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_MFMA SQ_WAVES && \
 timeout -k 10 300 python3 bench.py --steps 5 --warmup 2 --cpu-baseline off $EXTRA > $O/bench_pmcargs.json && \
-python3 tools/pmc_summary.py $O/pmc_fetch $O/pmc_write profiles/${TAG}_pmc_traffic.json $KEY 7 $CALIB && \
+python3 tools/pmc_summary.py $O/pmc_fetch $O/pmc_write profiles/${TAG}_pmc_traffic.json $KEY auto $CALIB && \
 python3 tools/pmc_sq_summary.py profiles/${TAG}_pmc_sq.json $KEY $O/pmc_sq1 $O/pmc_sq2 $O/pmc_sq1x $O/bench_pmcargs.json && \
 cp profiles/${TAG}_pmc_traffic.json profiles/${TAG}_pmc_sq.json $O/ && \
 timeout -k 10 300 python bench.py $EXTRA > $O/bench.json 2> $O/bench.err && \
