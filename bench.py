@@ -412,7 +412,8 @@ def main():
     kern_step_ms = kern_step_ms or float("nan")  # no timed launches (--kernel-timing off)
     achieved_tf = (flop_per_ray * rays_per_rank * executed_frac / (kern_step_ms * 1e-3) / 1e12
                    if have_stats else None)
-    key = f"{W}x{H}_M{M}_S{S}_V{vpg}" + ("_c16" if args.color_dtype == "f16" else "")
+    key = (f"{W}x{H}_M{M}_S{S}_V{vpg}" + ("_c16" if args.color_dtype == "f16" else "")
+           + (f"_k{K:g}" if K != 32.0 else ""))
     # per step (the step's launches together), like `achieved`; per launch where no per-step
     # summary exists for this workload
     traffic, traffic_src = _latest_profile("r*_pmc_traffic.json", key, "train_kernel_bytes_per_step")

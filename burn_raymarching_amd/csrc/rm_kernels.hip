@@ -2370,6 +2370,10 @@ struct FinalArgs {
 #define RM_REDUCE_BATCH 8
 #endif
 constexpr int kReduceBatch = RM_REDUCE_BATCH;  // partial rows in flight per thread
+#ifndef RM_FIN_U
+#define RM_FIN_U 16  // finalize_block: 4 * RM_FIN_U loads in flight (32 with batch 16: no gain at C2)
+#endif
+static_assert((kReduceSegs / 4) % RM_FIN_U == 0, "finalize_block rounds");
 
 __device__ void finalize_block(const float* S, int M, int Mpad, const FinalArgs& f, float* tot);
 
@@ -2443,8 +2447,8 @@ __device__ void finalize_block(const float* S, int M, int Mpad, const FinalArgs&
   const int tid = threadIdx.x;
   const int col = blockIdx.x * 256 + tid;
   const int c = min(col, ncols - 1);
-  // 64 loads in flight per thread (the last block runs alone: registers are free), two rounds
-  constexpr int kU = 16;
+  // kU * 4 loads in flight per thread (the last block runs alone: registers are free)
+  constexpr int kU = RM_FIN_U;
   float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   for (int u0 = 0; u0 < kReduceSegs / 4; u0 += kU) {
     float v[kU][4];
