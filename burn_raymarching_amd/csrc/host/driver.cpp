@@ -283,21 +283,30 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
         rmh_dataset_sample_count(ds.get(), share(q), uniform_ratio, &qu, &qf);
         n_global += qu + qf;
       }
-      RMCHK(g.ctx, rm_sample_batch(g.ctx, d_org.f(), d_dir.f(), d_tgt.f(), P, d_fg.i(), n_fg_list, n_uni, n_boost,
-                                   cfg->seed, sample_stream, (uint64_t)global_step, b_org.f(), b_dir.f(), b_tgt.f(),
-                                   nullptr));
       // model.forward + compute_loss + backward (train.rs:182-190), mean over the n*3 elements
       const float inv_count = 1.0f / (3.0f * (float)n_global);
-      RMCHK(g.ctx, rm_train_step(g.ctx, b_org.f(), b_dir.f(), b_tgt.f(), n, progress, inv_count, &sc, &march, &gr,
-                                 d_loss, nullptr, 0));
-      if (comm && (rc = comm->all_reduce_sum(comm->state, d_grad.f(), (int64_t)np + 1, g.stream)) != RMH_OK)
-        return fail(rc, "all-reduce of the gradient (stage %d, step %d): %s", stage, step, rmh_last_error());
       const double lr = step > cfg->steps_per_stage / 2 ? base_lr * 0.2 : base_lr;  // train.rs:193-197
       const bool last = stage == cfg->stages - 1 && step == cfg->steps_per_stage;
       const bool read_loss = (verbose && step % cfg->log_every == 0) || last;
-      // the penalty share of the loss costs a summation launch: only on the steps that report it
-      RMCHK(g.ctx, rm_optimizer_step(g.ctx, d_raw.f(), d_grad.f(), d_m.f(), d_v.f(), M, step, (float)lr,
-                                     cfg->weight_decay, 1, read_loss ? d_loss + 1 : nullptr, d_act.f()));
+      if (world == 1) {
+        // one process: draw + render + backward + optimizer in one call (one launch for the
+        // small models of the schedule; the penalty share is only summed on reporting steps)
+        RMCHK(g.ctx, rm_train_iteration(g.ctx, d_org.f(), d_dir.f(), d_tgt.f(), P, d_fg.i(), n_fg_list, n_uni, n_boost,
+                                        cfg->seed, sample_stream, (uint64_t)global_step, progress, inv_count, &march,
+                                        d_act.f(), d_grad.f(), d_raw.f(), d_m.f(), d_v.f(), M, step, (float)lr,
+                                        cfg->weight_decay, 1, d_loss, read_loss ? d_loss + 1 : nullptr));
+      } else {
+        RMCHK(g.ctx, rm_sample_batch(g.ctx, d_org.f(), d_dir.f(), d_tgt.f(), P, d_fg.i(), n_fg_list, n_uni, n_boost,
+                                     cfg->seed, sample_stream, (uint64_t)global_step, b_org.f(), b_dir.f(), b_tgt.f(),
+                                     nullptr));
+        RMCHK(g.ctx, rm_train_step(g.ctx, b_org.f(), b_dir.f(), b_tgt.f(), n, progress, inv_count, &sc, &march, &gr,
+                                   d_loss, nullptr, 0));
+        if ((rc = comm->all_reduce_sum(comm->state, d_grad.f(), (int64_t)np + 1, g.stream)) != RMH_OK)
+          return fail(rc, "all-reduce of the gradient (stage %d, step %d): %s", stage, step, rmh_last_error());
+        // the penalty share of the loss costs a summation launch: only on the steps that report it
+        RMCHK(g.ctx, rm_optimizer_step(g.ctx, d_raw.f(), d_grad.f(), d_m.f(), d_v.f(), M, step, (float)lr,
+                                       cfg->weight_decay, 1, read_loss ? d_loss + 1 : nullptr, d_act.f()));
+      }
       ++steps_done;
       if (read_loss) {
         float s[2];

@@ -2784,11 +2784,12 @@ __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restri
 // threads per sphere, their partials added in order), then optimizer_elem per element and the
 // penalty sum (block tree reduction). One launch instead of three.
 constexpr int kOptSmallMaxM = 64;
-__global__ __launch_bounds__(256) void rm_optimizer_small(float* __restrict__ raw, const float* __restrict__ gact,
-                                                          float* __restrict__ m1, float* __restrict__ m2, int M,
-                                                          int step, float lr, float wd, int with_pen,
-                                                          float* __restrict__ loss_penalty, float* __restrict__ act_out,
-                                                          _Float16* __restrict__ col_h_out) {
+// The body, for a 256-thread block (also the tail of the fused training iteration, rm_small.h).
+__device__ __forceinline__ void optimizer_small_block(float* __restrict__ raw, const float* gact,
+                                                      float* __restrict__ m1, float* __restrict__ m2, int M, int step,
+                                                      float lr, float wd, int with_pen,
+                                                      float* __restrict__ loss_penalty, float* __restrict__ act_out,
+                                                      _Float16* __restrict__ col_h_out) {
   __shared__ float snap[7 * kOptSmallMaxM + 4];
   __shared__ float part[4][kOptSmallMaxM][4];
   __shared__ float pair[kOptSmallMaxM * 4];
@@ -2822,6 +2823,14 @@ __global__ __launch_bounds__(256) void rm_optimizer_small(float* __restrict__ ra
   }
 }
 
+__global__ __launch_bounds__(256) void rm_optimizer_small(float* __restrict__ raw, const float* __restrict__ gact,
+                                                          float* __restrict__ m1, float* __restrict__ m2, int M,
+                                                          int step, float lr, float wd, int with_pen,
+                                                          float* __restrict__ loss_penalty, float* __restrict__ act_out,
+                                                          _Float16* __restrict__ col_h_out) {
+  optimizer_small_block(raw, gact, m1, m2, M, step, lr, wd, with_pen, loss_penalty, act_out, col_h_out);
+}
+
 __global__ void rm_sum_small(const float* __restrict__ parts, int n, float* __restrict__ out) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     float acc = 0.0f;
@@ -2851,6 +2860,8 @@ struct rm_context {
   void* rec = nullptr;                      // sphere records of the current call (rm_prep_kernel)
   unsigned* arrivals = nullptr;             // rm_small_kernel's arrival counter (zero between launches)
   unsigned* red_arrivals = nullptr;         // rm_reduce_partials' per-column-block arrival counters
+  float* batch = nullptr;                   // rm_train_iteration's unfused path: the drawn batch (9 floats/ray)
+  size_t batch_bytes = 0;
   size_t rec_bytes = 0;
   long long stats_blocks = 0;               // ray blocks launched while stats are on
   long long stats_waves = 0;                // their ray waves (a split block holds one)
@@ -3058,6 +3069,9 @@ struct Call {
   const rm_grads* grads = nullptr;
   float* loss_sum = nullptr;
   int accumulate = 0;
+  // rm_train_iteration: org / dir / targets are the dataset arrays the kernel draws the batch
+  // from, and the optimizer runs in the same launch (rm_small_kernel<kTrain, MB, true>)
+  const SmallArgs* fused = nullptr;
 };
 
 FinalArgs final_args(const Call& c, bool first) {
@@ -3131,19 +3145,19 @@ bool use_small(const Call& c, int M, long long n) {
 }
 
 // rm_small_kernel for M spheres: the bucket of M rounded up to a multiple of 4
-template <int MODE>
+template <int MODE, bool FUSED = false>
 void launch_small_m(int M, dim3 grid, hipStream_t st, const KArgs& a, const SmallArgs& sa, hipEvent_t ev0,
                     hipEvent_t ev1) {
   const dim3 blk(kBlock);
   switch ((M + 3) / 4) {
-    case 1: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 4>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
-    case 2: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 8>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
-    case 3: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 12>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
-    case 4: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 16>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
-    case 5: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 20>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
-    case 6: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 24>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
-    case 7: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 28>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
-    default: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 32>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    case 1: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 4, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    case 2: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 8, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    case 3: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 12, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    case 4: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 16, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    case 5: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 20, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    case 6: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 24, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    case 7: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 28, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    default: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 32, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
   }
 }
 
@@ -3165,9 +3179,12 @@ int run_small(rm_context* ctx, const Call& c, KArgs& a, long long n) {
     a.partials = static_cast<float*>(ctx->ws);
     SmallArgs sa;
     std::memset(&sa, 0, sizeof sa);
+    if (c.fused) sa = *c.fused;
     if (has_bwd) sa.fin = final_args(c, first);
     sa.arrivals = ctx->arrivals;
     sa.final_in_kernel = has_bwd && nb <= kSmallFinalMaxBlocks && !env_is("RM_SMALL_FINAL", '0') ? 1 : 0;
+    if (c.fused && (!sa.final_in_kernel || nr != n))  // rm_train_iteration checked this
+      return fail(ctx, RM_ERR_INVALID_ARG, "fused iteration needs one launch of <= %d blocks", kSmallFinalMaxBlocks);
     if (ctx->stats_dev) {
       ctx->stats_blocks += nb;
       ctx->stats_waves += nb * kWaves;
@@ -3175,7 +3192,8 @@ int run_small(rm_context* ctx, const Call& c, KArgs& a, long long n) {
     hipEvent_t ev0, ev1;
     if ((rc = next_events(ctx, ev0, ev1)) != RM_OK) return rc;
     const dim3 grid((unsigned)nb);
-    if (c.mode == kFwd) launch_small_m<kFwd>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
+    if (c.fused) launch_small_m<kTrain, true>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
+    else if (c.mode == kFwd) launch_small_m<kFwd>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
     else if (c.mode == kBwd) launch_small_m<kBwd>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
     else launch_small_m<kTrain>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
     RM_HIP(ctx, hipGetLastError());
@@ -3311,6 +3329,7 @@ int run(rm_context* ctx, const Call& c) {
   }
   a.rec = rec_floats(Mpad);
   if (use_small(c, M, n)) return run_small(ctx, c, a, n);
+  if (c.fused) return fail(ctx, RM_ERR_INVALID_ARG, "fused iteration outside the small kernel");
   // sphere records of this call (rm_prep_kernel): read by every sweep through scalar loads
   if (n > 0) {
     const int np = Mpad / 2, nprep = (np + 255) / 256;
@@ -3635,10 +3654,11 @@ void rm_destroy(rm_context* ctx) {
     if (ctx->ocnt) (void)hipFree(ctx->ocnt);
     if (ctx->rec) (void)hipFree(ctx->rec);
   }
-  if (ctx->arrivals || ctx->red_arrivals) {
+  if (ctx->arrivals || ctx->red_arrivals || ctx->batch) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->arrivals) (void)hipFree(ctx->arrivals);
     if (ctx->red_arrivals) (void)hipFree(ctx->red_arrivals);
+    if (ctx->batch) (void)hipFree(ctx->batch);
   }
   for (auto& pr : ctx->events) {
     (void)hipEventDestroy(pr.first);
@@ -3863,6 +3883,23 @@ int rm_gather_rays(rm_context* ctx, const float* ray_org, const float* ray_dir, 
   return RM_OK;
 }
 
+}  // extern "C"
+
+namespace {
+// the sampler's per-call key: (seed, stream, counter) mixed on the host
+unsigned long long sample_key(uint64_t seed, uint64_t stream, uint64_t counter) {
+  auto mix = [](unsigned long long z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+  };
+  return mix(mix(mix(seed) ^ stream) ^ counter);
+}
+}  // namespace
+
+extern "C" {
+
 int rm_sample_batch(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets, int64_t num_src,
                     const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform, int64_t n_fg, uint64_t seed,
                     uint64_t stream, uint64_t counter, float* out_org, float* out_dir, float* out_targets,
@@ -3876,14 +3913,7 @@ int rm_sample_batch(rm_context* ctx, const float* ray_org, const float* ray_dir,
   if ((out_org && !ray_org) || (out_dir && !ray_dir) || (out_targets && !targets))
     return fail(ctx, RM_ERR_INVALID_ARG, "an output is requested without its source array");
   if (!out_org && !out_dir && !out_targets && !indices_out) return fail(ctx, RM_ERR_INVALID_ARG, "no output requested");
-  // the call's key: (seed, stream, counter) mixed on the host
-  auto mix = [](unsigned long long z) {
-    z += 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-  };
-  const unsigned long long key = mix(mix(mix(seed) ^ stream) ^ counter);
+  const unsigned long long key = sample_key(seed, stream, counter);
   hipLaunchKernelGGL(rm::rm_sample_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, ray_org, ray_dir,
                      targets, (long long)num_src, fg_indices, (long long)num_fg, (long long)n_uniform, n, key, out_org,
                      out_dir, out_targets, indices_out);
@@ -3954,6 +3984,98 @@ int rm_optimizer_step(rm_context* ctx, float* raw_packed, const float* grad_act_
                       int32_t with_penalties, float* loss_penalty, float* act_out) {
   return rm_optimizer_step_f16(ctx, raw_packed, grad_act_packed, adam_m, adam_v, num_spheres, step, lr, weight_decay,
                                with_penalties, loss_penalty, act_out, nullptr);
+}
+
+int rm_train_iteration(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
+                       int64_t num_src, const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform, int64_t n_fg,
+                       uint64_t seed, uint64_t stream, uint64_t counter, float progress, float inv_count,
+                       const rm_march* march, float* act_packed, float* grad_packed, float* raw_packed,
+                       float* adam_m, float* adam_v, int32_t num_spheres, int32_t step, float lr,
+                       float weight_decay, int32_t with_penalties, float* loss_sum, float* loss_penalty) {
+  if (!ctx) return RM_ERR_INVALID_ARG;
+  if (!ray_org || !ray_dir || !targets) return fail(ctx, RM_ERR_INVALID_ARG, "NULL dataset array");
+  if (!act_packed || !grad_packed || !raw_packed || !adam_m || !adam_v || !march)
+    return fail(ctx, RM_ERR_INVALID_ARG, "NULL model buffer");
+  if (num_spheres < 1 || num_spheres > RM_MAX_SPHERES) return fail(ctx, RM_ERR_INVALID_ARG, "bad num_spheres");
+  if ((march->flags & RM_MARCH_COLOR_F16) != 0)
+    return fail(ctx, RM_ERR_INVALID_ARG, "rm_train_iteration trains fp32 colour models");
+  if (num_src < 1 || num_src > INT32_MAX || n_uniform < 0 || n_fg < 0 || num_fg < 0)
+    return fail(ctx, RM_ERR_INVALID_ARG, "bad sampling sizes");
+  if (n_fg > 0 && (num_fg == 0 || !fg_indices)) return fail(ctx, RM_ERR_INVALID_ARG, "n_fg > 0 needs foreground indices");
+  if (step < 1) return fail(ctx, RM_ERR_INVALID_ARG, "step counts from 1");
+  const int M = num_spheres;
+  const long long n = n_uniform + n_fg;
+  rm_scene sc;
+  rm_scene_from_packed(act_packed, M, &sc);
+  rm_grads gr;
+  rm_grads_from_packed(grad_packed, M, &gr);
+  Call c;
+  c.mode = kTrain;
+  c.cam = false;
+  c.org = ray_org;
+  c.dir = ray_dir;
+  c.n = n;
+  c.targets = targets;
+  c.progress = progress;
+  c.inv_count = inv_count;
+  c.scene = &sc;
+  c.march = march;
+  c.grads = &gr;
+  c.loss_sum = loss_sum;
+  c.accumulate = 0;
+  // one launch: the small kernel with its in-kernel final reduction (RM_FUSED_ITER=0: three calls)
+  const bool fused = use_small(c, M, n) && (n + kBlock - 1) / kBlock <= kSmallFinalMaxBlocks &&
+                     (n + kBlock - 1) / kBlock <= max_blocks_per_launch() &&
+                     M <= kOptSmallMaxM && !env_is("RM_SMALL_FINAL", '0') &&
+                     !env_is("RM_FUSED_ITER", '0');
+  if (fused) {
+    SmallArgs fz;
+    std::memset(&fz, 0, sizeof fz);
+    fz.src_org = ray_org;
+    fz.src_dir = ray_dir;
+    fz.src_tgt = targets;
+    fz.fg = fg_indices;
+    fz.num_src = num_src;
+    fz.num_fg = num_fg;
+    fz.n_uniform = n_uniform;
+    fz.key = sample_key(seed, stream, counter);
+    fz.raw = raw_packed;
+    fz.m1 = adam_m;
+    fz.m2 = adam_v;
+    fz.step = step;
+    fz.with_pen = with_penalties ? 1 : 0;
+    fz.lr = lr;
+    fz.wd = weight_decay;
+    fz.loss_penalty = loss_penalty;
+    fz.act_out = act_packed;
+    c.fused = &fz;
+    return run(ctx, c);
+  }
+  // the same three steps as separate calls: draw + gather, train step, optimizer
+  int rc;
+  if (n > 0) {
+    const size_t need = sizeof(float) * 9 * (size_t)n;
+    if (need > ctx->batch_bytes) {
+      if (ctx->batch) {
+        RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        RM_HIP(ctx, hipFree(ctx->batch));
+        ctx->batch = nullptr;
+        ctx->batch_bytes = 0;
+      }
+      if (hipMalloc(&ctx->batch, need) != hipSuccess) return fail(ctx, RM_ERR_OOM, "batch buffer (%zu B)", need);
+      ctx->batch_bytes = need;
+    }
+  }
+  float* bo = ctx->batch;
+  float* bd = bo ? bo + 3 * n : nullptr;
+  float* bt = bo ? bo + 6 * n : nullptr;
+  if (n > 0 && (rc = rm_sample_batch(ctx, ray_org, ray_dir, targets, num_src, fg_indices, num_fg, n_uniform, n_fg, seed,
+                                     stream, counter, bo, bd, bt, nullptr)) != RM_OK)
+    return rc;
+  if ((rc = rm_train_step(ctx, bo, bd, bt, n, progress, inv_count, &sc, march, &gr, loss_sum, nullptr, 0)) != RM_OK)
+    return rc;
+  return rm_optimizer_step(ctx, raw_packed, grad_packed, adam_m, adam_v, M, step, lr, weight_decay, with_penalties,
+                           loss_penalty, act_packed);
 }
 
 }  // extern "C"

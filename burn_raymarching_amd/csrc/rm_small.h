@@ -22,6 +22,8 @@
 //  * the backward keeps one ray per lane and sums each sphere's seven gradient terms over the
 //    wave with the transposing 8-value reduction (wave_reduce8), the four waves in LDS in order.
 // Deterministic: every sum has a fixed order (lanes, waves, blocks).
+// FUSED (rm_train_iteration): the reference loop's whole step in this one launch -- the batch drawn
+// and gathered per ray, and the optimizer step run by the last block after the gradient sums.
 #pragma once
 
 constexpr int kSmallMaxM = 32;             // spheres handled by the small kernel
@@ -31,6 +33,22 @@ struct SmallArgs {
   FinalArgs fin;          // where the last block writes the gradients and the loss
   unsigned* arrivals;     // arrival counter (zero between launches; the last block resets it)
   int final_in_kernel;    // 1: the last block reduces and finalizes; 0: partial records only
+  // The fused training iteration (rm_train_iteration; kernel template FUSED): the batch is drawn
+  // and gathered in the kernel (rm_sample_kernel's rows: ray i of the call reads row j of the
+  // dataset arrays) and the last block runs the optimizer step on the gradient it has summed.
+  const float* src_org;
+  const float* src_dir;
+  const float* src_tgt;
+  const int32_t* fg;
+  long long num_src, num_fg, n_uniform;
+  unsigned long long key;
+  float* raw;             // optimizer (optimizer_small_block): raw parameters, moments
+  float* m1;
+  float* m2;
+  int step, with_pen;
+  float lr, wd;
+  float* loss_penalty;    // nullable
+  float* act_out;         // the next render's activated parameters (the scene this launch read)
 };
 
 // Per-sphere march data in registers, pair p = spheres (2p, 2p + 1): gx = -2c, cc = |c|^2
@@ -66,9 +84,10 @@ __device__ __forceinline__ float small_softmin(const float p[3], const SmallSphe
   return -(flog2(fmaxf(s, 1e-8f)) + m) * inv_kappa;
 }
 
-template <int MODE, int MB>
+template <int MODE, int MB, bool FUSED = false>
 __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, const SmallArgs sa) {
   static_assert(MB % 2 == 0 && MB <= kSmallMaxM, "sphere bucket");
+  static_assert(!FUSED || MODE == kTrain, "the fused iteration is a train step");
   constexpr int kRec = kSmallMaxM * 8 + 8;  // per-wave slot of the cross-wave sums
   constexpr int NP = MB / 2;
   __shared__ float4 s_geo[MB];              // {gx, gy, gz, cc}
@@ -105,8 +124,22 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
   long long ri = a.ray_begin + (valid ? li : 0);
   float o[3], d[3];
   int view;
-  if (a.num_views > 0) setup_ray<true>(a, ri, o, d, view);
-  else setup_ray<false>(a, ri, o, d, view);
+  long long ti;  // the row of the target (setup_ray turns ri into the ray's row)
+  if constexpr (FUSED) {  // SceneDataset::sample_batch (dataset.rs:47-82), as rm_sample_kernel
+    const unsigned long long r = splitmix64(sa.key + (unsigned long long)(ri + 1) * 0x9E3779B97F4A7C15ull);
+    const long long j = ri < sa.n_uniform ? (long long)__umul64hi(r, (unsigned long long)sa.num_src)
+                                          : (long long)sa.fg[__umul64hi(r, (unsigned long long)sa.num_fg)];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      o[c] = sa.src_org[3 * j + c];
+      d[c] = sa.src_dir[3 * j + c];
+    }
+    ti = j;
+  } else {
+    if (a.num_views > 0) setup_ray<true>(a, ri, o, d, view);
+    else setup_ray<false>(a, ri, o, d, view);
+    ti = ri;
+  }
   __syncthreads();
   SmallSpheres<MB> S;
 #pragma unroll
@@ -209,7 +242,8 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
       g[1] = a.gout[3 * ri + 1];
       g[2] = a.gout[3 * ri + 2];
     } else {
-      const float t0 = a.targets[3 * ri], t1 = a.targets[3 * ri + 1], t2 = a.targets[3 * ri + 2];
+      const float* tgt = FUSED ? sa.src_tgt : a.targets;
+      const float t0 = tgt[3 * ti], t1 = tgt[3 * ti + 1], t2 = tgt[3 * ti + 2];
       const float W = (t0 + t1 + t2) > 0.01f ? 10.0f : fmaf(a.progress, 4.0f, 1.0f);
       const float tg[3] = {t0, t1, t2};
 #pragma unroll
@@ -385,5 +419,14 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
     if (f.gamb) f.gamb[0] = f.accumulate ? f.gamb[0] + sc[3] : sc[3];
     if (f.loss_sum) f.loss_sum[0] = f.accumulate ? f.loss_sum[0] + sc[4] : sc[4];
     __hip_atomic_store(sa.arrivals, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+  }
+  if constexpr (FUSED) {
+    // the optimizer step (rm_optimizer_step: penalties + Adam, train.rs:198) on the gradient just
+    // written -- from this block's own stores (visible to the block after the barrier), in the
+    // packed layout the optimizer reads. Every other block has arrived, so nothing reads the
+    // activated parameters any more when act_out overwrites them.
+    __syncthreads();
+    optimizer_small_block(sa.raw, f.gc, sa.m1, sa.m2, M, sa.step, sa.lr, sa.wd, sa.with_pen, sa.loss_penalty,
+                          sa.act_out, nullptr);
   }
 }

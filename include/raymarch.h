@@ -308,6 +308,28 @@ int rm_optimizer_step_f16(rm_context* ctx, float* raw_packed, const float* grad_
                           float* adam_v, int32_t num_spheres, int32_t step, float lr, float weight_decay,
                           int32_t with_penalties, float* loss_penalty, float* act_out, uint16_t* colors_f16_out);
 
+/* One step of the reference training loop (train.rs:169-198) for one process, replacing the
+ * sequence rm_sample_batch -> rm_train_step -> rm_optimizer_step with the same arguments and
+ * the same results bit for bit:
+ *   1. the batch: rows drawn from the dataset arrays ray_org / ray_dir / targets ([num_src,3])
+ *      as rm_sample_batch draws them (n_uniform + n_fg rows; seed, stream, counter);
+ *   2. the render of the scene act_packed (activated packed parameters), the loss seed and the
+ *      backward into grad_packed ((7M+4) floats, overwritten) and loss_sum (1 float, overwritten),
+ *      as rm_train_step with progress, inv_count and march;
+ *   3. the optimizer step on raw_packed / adam_m / adam_v (step, lr, weight_decay,
+ *      with_penalties, loss_penalty nullable) writing the updated activated parameters back into
+ *      act_packed, as rm_optimizer_step with act_out = act_packed.
+ * Models of up to 32 spheres and batches of up to 32,768 rays run as ONE launch (the small-scene
+ * kernel draws and gathers its rays and its last block runs the optimizer; env
+ * RM_FUSED_ITER=0 turns this off); other sizes run the three calls. fp32 colour models only.
+ * Not for data-parallel training: the gradient is consumed before it could be all-reduced. */
+int rm_train_iteration(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
+                       int64_t num_src, const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform, int64_t n_fg,
+                       uint64_t seed, uint64_t stream, uint64_t counter, float progress, float inv_count,
+                       const rm_march* march, float* act_packed, float* grad_packed, float* raw_packed,
+                       float* adam_m, float* adam_v, int32_t num_spheres, int32_t step, float lr,
+                       float weight_decay, int32_t with_penalties, float* loss_sum, float* loss_penalty);
+
 #ifdef __cplusplus
 }
 #endif

@@ -209,3 +209,74 @@ def test_small_and_general_kernel_agree(rm, oracle, monkeypatch):
     for key in KEYS:
         a, b = res["1"][1][key], res["0"][1][key]
         assert np.abs(a - b).max() <= 3e-3 * max(np.abs(b).max(), 1e-12), key
+
+
+def _iteration(torch, native, render, model, src, fg, nu, nf, sc, steps, fused, monkeypatch):
+    """`steps` training iterations (train.rs:169-198) through rm_train_iteration (fused: one launch
+    when eligible) or through rm_sample_batch + rm_train_step + rm_optimizer_step."""
+    import ctypes
+    monkeypatch.setenv("RM_FUSED_ITER", "1" if fused else "0")
+    m = sc["centers"].shape[0]
+    sm = model.SceneModel.from_activated(sc["centers"], sc["colors"], sc["radius"], sc["light_dir"], sc["ambient"])
+    raw = sm.raw.clone()
+    act = sm.activated_packed().clone()
+    npk = model.packed_size(m)
+    grad = torch.zeros(npk, device="cuda")
+    mom = [torch.zeros(npk, device="cuda") for _ in range(2)]
+    loss = torch.zeros(2, device="cuda")
+    ctx = render.context()
+    p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    o, d, t = src
+    n = nu + nf
+    out = []
+    for it in range(1, steps + 1):
+        k = 5.0 + 27.0 * it / steps
+        march = native.march_params(40, k)
+        args = (o.shape[0], p(fg), fg.numel(), nu, nf, 11, 1, it, it / steps, 1.0 / (3 * n))
+        if fused:
+            ctx.check(ctx._lib.rm_train_iteration(ctx.handle, p(o), p(d), p(t), *args, ctypes.byref(march), p(act),
+                                                  p(grad), p(raw), p(mom[0]), p(mom[1]), m, it, 0.01, 1e-5, 1,
+                                                  p(loss), ctypes.c_void_p(loss.data_ptr() + 4)), "rm_train_iteration")
+        else:
+            b = [torch.empty((n, 3), device="cuda") for _ in range(3)]
+            ctx.check(ctx._lib.rm_sample_batch(ctx.handle, p(o), p(d), p(t), *args[:8], p(b[0]), p(b[1]), p(b[2]),
+                                               None), "rm_sample_batch")
+            s = native.RmScene()
+            ctx._lib.rm_scene_from_packed(p(act), m, ctypes.byref(s))
+            g = native.RmGrads()
+            ctx._lib.rm_grads_from_packed(p(grad), m, ctypes.byref(g))
+            ctx.check(ctx._lib.rm_train_step(ctx.handle, p(b[0]), p(b[1]), p(b[2]), n, it / steps, 1.0 / (3 * n),
+                                             ctypes.byref(s), ctypes.byref(march), ctypes.byref(g), p(loss), None, 0),
+                      "rm_train_step")
+            ctx.check(ctx._lib.rm_optimizer_step(ctx.handle, p(raw), p(grad), p(mom[0]), p(mom[1]), m, it, 0.01, 1e-5, 1,
+                                                 ctypes.c_void_p(loss.data_ptr() + 4), p(act)), "rm_optimizer_step")
+            torch.cuda.synchronize()
+        out.append([x.clone() for x in (raw, act, grad, mom[0], mom[1], loss)])
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("m,nu,nf", [(7, 13107, 3277), (20, 9000, 7384), (32, 30000, 2768), (40, 13107, 3277),
+                                     (9, 40000, 0)])
+def test_train_iteration_equals_three_calls(rm, oracle, monkeypatch, m, nu, nf):
+    """rm_train_iteration = rm_sample_batch -> rm_train_step -> rm_optimizer_step, bit for bit, over
+    five iterations with penalties and k annealed (train.rs:169-198). One launch for M <= 32 and
+    <= 32,768 rays; M = 40 and 40,000 rays run the three calls inside the entry point."""
+    import torch
+    render, model, native = rm
+    rng = np.random.default_rng(m)
+    cams = model.ring_cameras(4)
+    rays = [oracle.camera_rays(64, 64, *c, precision="f32") for c in cams]
+    o = np.concatenate([r[0] for r in rays])
+    d = np.concatenate([r[1] for r in rays])
+    tg = oracle.render_diff(o.astype(np.float64), d.astype(np.float64), train_scene(model, 6, 2), 24, 32.0)
+    src = [dev(o), dev(d), dev(tg)]
+    fg = torch.from_numpy(np.flatnonzero(tg.sum(1) > 0.01).astype(np.int32)).cuda()
+    sc = train_scene(model, m, 40 + m)
+    a = _iteration(torch, native, render, model, src, fg, nu, nf, sc, 5, True, monkeypatch)
+    b = _iteration(torch, native, render, model, src, fg, nu, nf, sc, 5, False, monkeypatch)
+    names = ("raw", "act", "grad", "adam_m", "adam_v", "loss")
+    for it, (xa, xb) in enumerate(zip(a, b)):
+        for name, u, v in zip(names, xa, xb):
+            assert torch.equal(u, v), (it, name, (u - v).abs().max().item())
+    assert torch.isfinite(a[-1][0]).all() and a[-1][5][0] > 0
