@@ -288,9 +288,9 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
       const double lr = step > cfg->steps_per_stage / 2 ? base_lr * 0.2 : base_lr;  // train.rs:193-197
       const bool last = stage == cfg->stages - 1 && step == cfg->steps_per_stage;
       const bool read_loss = (verbose && step % cfg->log_every == 0) || last;
-      if (world == 1) {
-        // one process: draw + render + backward + optimizer in one call (one launch for the
-        // small models of the schedule; the penalty share is only summed on reporting steps)
+      if (!comm) {
+        // one process, no collective: draw + render + backward + optimizer in one call (one
+        // launch for the small models of the schedule; the penalty share only on reporting steps)
         RMCHK(g.ctx, rm_train_iteration(g.ctx, d_org.f(), d_dir.f(), d_tgt.f(), P, d_fg.i(), n_fg_list, n_uni, n_boost,
                                         cfg->seed, sample_stream, (uint64_t)global_step, progress, inv_count, &march,
                                         d_act.f(), d_grad.f(), d_raw.f(), d_m.f(), d_v.f(), M, step, (float)lr,
