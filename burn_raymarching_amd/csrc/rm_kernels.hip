@@ -3132,16 +3132,21 @@ int next_events(rm_context* ctx, hipEvent_t& ev0, hipEvent_t& ev1) {
 }
 
 // Small scenes (M <= kSmallMaxM): rm_small_kernel. Taken by default for ray-array calls (the
-// reference training loop's random batches, train.rs:169-199); env RM_SMALL=1 takes it for every
-// eligible call (camera mode too), RM_SMALL=0 never. Not for the renderer.rs mode, the diagnostics
-// or the flags that select the general kernel's march paths for testing.
+// reference training loop's random batches, train.rs:169-199) and for camera calls of up to
+// kSmallCamMaxRays rays (64x64 / 16 steps: 13.5 vs 56 us, 256x256 / 40 steps: 25 vs 84 us;
+// tools/small_batch_sweep.py -- larger camera calls keep the general kernel's exact early exits);
+// env RM_SMALL=1 takes it for every eligible call, RM_SMALL=0 never. Not for the renderer.rs
+// mode, the diagnostics or the flags that select the general kernel's march paths for testing.
+constexpr long long kSmallCamMaxRays = 1LL << 20;
 bool use_small(const Call& c, int M, long long n) {
   if (M > kSmallMaxM || n <= 0 || c.mode == kRender || c.dbg) return false;
-  if ((c.march->flags & (RM_MARCH_VALU_ONLY | RM_MARCH_FORCE_MAX_SHIFT | RM_MARCH_SPLIT)) != 0) return false;
+  if ((c.march->flags & (RM_MARCH_VALU_ONLY | RM_MARCH_FORCE_MAX_SHIFT | RM_MARCH_SPLIT | RM_MARCH_PER_RAY_ORIGIN |
+                         RM_MARCH_SKIP_ESCAPED)) != 0)
+    return false;
   const char* e = std::getenv("RM_SMALL");
   if (e && e[0] == '0') return false;
   if (e && e[0] == '1') return true;
-  return !c.cam;
+  return !c.cam || n <= kSmallCamMaxRays;
 }
 
 // rm_small_kernel for M spheres: the bucket of M rounded up to a multiple of 4

@@ -20,6 +20,9 @@ def mods():
 
 
 def _both(monkeypatch, fn):
+    # the general kernel's origin step (small camera calls of <= 32 spheres otherwise take the
+    # small-scene kernel, which marches every step per ray)
+    monkeypatch.setenv("RM_SMALL", "0")
     monkeypatch.setenv("RM_PER_RAY_ORIGIN", "1")
     per_ray = fn()
     monkeypatch.setenv("RM_PER_RAY_ORIGIN", "0")
