@@ -2692,10 +2692,10 @@ __global__ __launch_bounds__(256) void rm_penalty_pairs(const float* __restrict_
 // parameters (a snapshot: neighbours are read); pair: the repulsion rows. Returns the element's
 // penalty-loss share.
 __device__ __forceinline__ float optimizer_elem(int i, const float* raw, float* __restrict__ raw_out,
-                                                const float* __restrict__ gact, float* __restrict__ m1,
-                                                float* __restrict__ m2, const float* pair, int M, int step, float lr,
-                                                float wd, int with_pen, float* __restrict__ act_out,
-                                                _Float16* __restrict__ col_h_out) {
+                                                const float* __restrict__ gact, const float* m1_in,
+                                                const float* m2_in, float* __restrict__ m1, float* __restrict__ m2,
+                                                const float* pair, int M, int step, float lr, float wd, int with_pen,
+                                                float* __restrict__ act_out, _Float16* __restrict__ col_h_out) {
   float pen = 0.0f;
   const float x = raw[i];
   float gv = gact[i];
@@ -2744,8 +2744,8 @@ __device__ __forceinline__ float optimizer_elem(int i, const float* raw, float* 
   // Burn Adam with coupled weight decay: g += wd * theta; moments; bias correction.
   gv = fmaf(wd, x, gv);
   const float b1 = 0.9f, b2 = 0.999f, eps = 1e-5f;
-  const float mm = fmaf(b1, m1[i], (1.0f - b1) * gv);
-  const float vv = fmaf(b2, m2[i], (1.0f - b2) * gv * gv);
+  const float mm = fmaf(b1, m1_in[i], (1.0f - b1) * gv);
+  const float vv = fmaf(b2, m2_in[i], (1.0f - b2) * gv * gv);
   m1[i] = mm;
   m2[i] = vv;
   const float mh = mm / (1.0f - powf(b1, (float)step));
@@ -2771,7 +2771,8 @@ __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restri
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int n = 7 * M + 4;
   float pen = 0.0f;
-  if (i < n) pen = optimizer_elem(i, raw, raw_out, gact, m1, m2, pair, M, step, lr, wd, with_pen, act_out, col_h_out);
+  if (i < n)
+    pen = optimizer_elem(i, raw, raw_out, gact, m1, m2, m1, m2, pair, M, step, lr, wd, with_pen, act_out, col_h_out);
   if (pen_parts != nullptr) {
     float v[4] = {pen, 0.0f, 0.0f, 0.0f};
     block_sum4(v, red);
@@ -2780,23 +2781,53 @@ __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restri
 }
 
 // The optimizer step of a small model (M <= kOptSmallMaxM) in one block: the pre-step parameters
-// into LDS (the snapshot rm_penalty_pairs writes), the repulsion rows of training.rs:73-82 (four
-// threads per sphere, their partials added in order), then optimizer_elem per element and the
-// penalty sum (block tree reduction). One launch instead of three.
+// and moments into LDS (the snapshot rm_penalty_pairs writes), the repulsion rows of
+// training.rs:73-82 (four threads per sphere, their partials added in order), then optimizer_elem
+// per element and the penalty sum (block tree reduction). One launch instead of three.
+// OptPrefetch: the block's loads of the parameters and moments (elements tid and tid + 256),
+// issued before whatever the block does next (the fused iteration's final reduction) so that
+// their latency overlaps it.
 constexpr int kOptSmallMaxM = 64;
+struct OptPrefetch {
+  float x[2], a[2], b[2];
+};
+__device__ __forceinline__ OptPrefetch opt_prefetch(const float* raw, const float* m1, const float* m2, int M) {
+  OptPrefetch f;
+  const int n = 7 * M + 4;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = (int)threadIdx.x + 256 * h;
+    f.x[h] = i < n ? raw[i] : 0.0f;
+    f.a[h] = i < n ? m1[i] : 0.0f;
+    f.b[h] = i < n ? m2[i] : 0.0f;
+  }
+  return f;
+}
+
 // The body, for a 256-thread block (also the tail of the fused training iteration, rm_small.h).
-__device__ __forceinline__ void optimizer_small_block(float* __restrict__ raw, const float* gact,
-                                                      float* __restrict__ m1, float* __restrict__ m2, int M, int step,
-                                                      float lr, float wd, int with_pen,
-                                                      float* __restrict__ loss_penalty, float* __restrict__ act_out,
-                                                      _Float16* __restrict__ col_h_out) {
+__device__ __forceinline__ void optimizer_small_block(const OptPrefetch& pf, float* __restrict__ raw,
+                                                      const float* gact, float* __restrict__ m1,
+                                                      float* __restrict__ m2, int M, int step, float lr, float wd,
+                                                      int with_pen, float* __restrict__ loss_penalty,
+                                                      float* __restrict__ act_out, _Float16* __restrict__ col_h_out) {
+  static_assert(7 * kOptSmallMaxM + 4 <= 512, "two elements per thread");
   __shared__ float snap[7 * kOptSmallMaxM + 4];
+  __shared__ float sm1[7 * kOptSmallMaxM + 4];
+  __shared__ float sm2[7 * kOptSmallMaxM + 4];
   __shared__ float part[4][kOptSmallMaxM][4];
   __shared__ float pair[kOptSmallMaxM * 4];
   __shared__ float red[4 * 256];
   const int tid = threadIdx.x;
   const int n = 7 * M + 4;
-  for (int i = tid; i < n; i += 256) snap[i] = raw[i];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = tid + 256 * h;
+    if (i < n) {
+      snap[i] = pf.x[h];
+      sm1[i] = pf.a[h];
+      sm2[i] = pf.b[h];
+    }
+  }
   __syncthreads();
   if (with_pen) {
     const int s = tid >> 2, k = tid & 3;  // sphere s, columns j = k mod 4
@@ -2815,7 +2846,7 @@ __device__ __forceinline__ void optimizer_small_block(float* __restrict__ raw, c
   }
   float pen = 0.0f;
   for (int i = tid; i < n; i += 256)
-    pen += optimizer_elem(i, snap, raw, gact, m1, m2, pair, M, step, lr, wd, with_pen, act_out, col_h_out);
+    pen += optimizer_elem(i, snap, raw, gact, sm1, sm2, m1, m2, pair, M, step, lr, wd, with_pen, act_out, col_h_out);
   if (loss_penalty != nullptr) {
     float v[4] = {pen, 0.0f, 0.0f, 0.0f};
     block_sum4(v, red);
@@ -2828,7 +2859,8 @@ __global__ __launch_bounds__(256) void rm_optimizer_small(float* __restrict__ ra
                                                           int step, float lr, float wd, int with_pen,
                                                           float* __restrict__ loss_penalty, float* __restrict__ act_out,
                                                           _Float16* __restrict__ col_h_out) {
-  optimizer_small_block(raw, gact, m1, m2, M, step, lr, wd, with_pen, loss_penalty, act_out, col_h_out);
+  optimizer_small_block(opt_prefetch(raw, m1, m2, M), raw, gact, m1, m2, M, step, lr, wd, with_pen, loss_penalty,
+                        act_out, col_h_out);
 }
 
 __global__ void rm_sum_small(const float* __restrict__ parts, int n, float* __restrict__ out) {
@@ -3150,26 +3182,39 @@ bool use_small(const Call& c, int M, long long n) {
 }
 
 // rm_small_kernel for M spheres: the bucket of M rounded up to a multiple of 4
-template <int MODE, bool FUSED = false>
+template <int MODE, bool FUSED = false, int LPR = 1>
 void launch_small_m(int M, dim3 grid, hipStream_t st, const KArgs& a, const SmallArgs& sa, hipEvent_t ev0,
                     hipEvent_t ev1) {
   const dim3 blk(kBlock);
   switch ((M + 3) / 4) {
-    case 1: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 4, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
-    case 2: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 8, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
-    case 3: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 12, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
-    case 4: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 16, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
-    case 5: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 20, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
-    case 6: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 24, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
-    case 7: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 28, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
-    default: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 32, FUSED>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+#define RM_SMALL_CASE(C, MB) \
+  case C: hipExtLaunchKernelGGL((rm_small_kernel<MODE, MB, FUSED, LPR>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
+    RM_SMALL_CASE(1, 4)
+    RM_SMALL_CASE(2, 8)
+    RM_SMALL_CASE(3, 12)
+    RM_SMALL_CASE(4, 16)
+    RM_SMALL_CASE(5, 20)
+    RM_SMALL_CASE(6, 24)
+    RM_SMALL_CASE(7, 28)
+#undef RM_SMALL_CASE
+    default: hipExtLaunchKernelGGL((rm_small_kernel<MODE, 32, FUSED, LPR>), grid, blk, 0, st, ev0, ev1, 0u, a, sa); break;
   }
+}
+
+// Lanes per ray of a small-kernel call: train steps of up to 32,768 rays split each ray's march
+// over two lanes (rm_small.h, LPR; 16,384 rays: 18.6 vs 19.7 us, 4,096: 15.9 vs 19.2; from
+// 65,536 rays the SIMDs are full and one lane per ray is faster, 25.6 vs 28.7). Env
+// RM_SMALL_LPR=1 / 2 forces one or two.
+int small_lpr(const Call& c, long long n) {
+  if (c.mode != kTrain || env_is("RM_SMALL_LPR", '1')) return 1;
+  return env_is("RM_SMALL_LPR", '2') || n <= 32768 ? 2 : 1;
 }
 
 int run_small(rm_context* ctx, const Call& c, KArgs& a, long long n) {
   const bool has_bwd = c.mode == kBwd || c.mode == kTrain;
+  const int lpr = small_lpr(c, n), rpb = kBlock / lpr;
   int rc;
-  if (has_bwd && (rc = ensure_ws(ctx, ws_need(n, a.M))) != RM_OK) return rc;
+  if (has_bwd && (rc = ensure_ws(ctx, ws_need(n, a.M, rpb))) != RM_OK) return rc;
   if (!ctx->arrivals) {
     RM_HIP(ctx, hipMalloc(&ctx->arrivals, 64));
     RM_HIP(ctx, hipMemsetAsync(ctx->arrivals, 0, 64, ctx->stream));
@@ -3177,17 +3222,25 @@ int run_small(rm_context* ctx, const Call& c, KArgs& a, long long n) {
   long long done = 0;
   bool first = true;
   while (done < n) {
-    const long long nb = std::min<long long>((n - done + kBlock - 1) / kBlock, max_blocks_per_launch());
-    const long long nr = std::min<long long>(n - done, nb * kBlock);
+    const long long nb = std::min<long long>((n - done + rpb - 1) / rpb, max_blocks_per_launch());
+    const long long nr = std::min<long long>(n - done, nb * rpb);
     a.ray_begin = done;
     a.n_rays = nr;
     a.partials = static_cast<float*>(ctx->ws);
+#ifdef RM_BLOCK_TRACE
+    if (!ctx->btrace)
+      RM_HIP(ctx, hipMalloc(&ctx->btrace, sizeof(unsigned long long) * kTraceWords * kWaves * (size_t)kMaxBlocksPerLaunch));
+    RM_HIP(ctx, hipMemsetAsync(ctx->btrace, 0, sizeof(unsigned long long) * kTraceWords * kWaves * (size_t)nb, ctx->stream));
+    a.btrace = ctx->btrace;
+    ctx->btrace_waves = nb * kWaves;
+#endif
     SmallArgs sa;
     std::memset(&sa, 0, sizeof sa);
     if (c.fused) sa = *c.fused;
     if (has_bwd) sa.fin = final_args(c, first);
     sa.arrivals = ctx->arrivals;
     sa.final_in_kernel = has_bwd && nb <= kSmallFinalMaxBlocks && !env_is("RM_SMALL_FINAL", '0') ? 1 : 0;
+    sa.acquire = env_is("RM_SMALL_ACQUIRE", '0') ? 0 : 1;
     if (c.fused && (!sa.final_in_kernel || nr != n))  // rm_train_iteration checked this
       return fail(ctx, RM_ERR_INVALID_ARG, "fused iteration needs one launch of <= %d blocks", kSmallFinalMaxBlocks);
     if (ctx->stats_dev) {
@@ -3197,9 +3250,11 @@ int run_small(rm_context* ctx, const Call& c, KArgs& a, long long n) {
     hipEvent_t ev0, ev1;
     if ((rc = next_events(ctx, ev0, ev1)) != RM_OK) return rc;
     const dim3 grid((unsigned)nb);
-    if (c.fused) launch_small_m<kTrain, true>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
+    if (c.fused && lpr == 2) launch_small_m<kTrain, true, 2>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
+    else if (c.fused) launch_small_m<kTrain, true>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
     else if (c.mode == kFwd) launch_small_m<kFwd>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
     else if (c.mode == kBwd) launch_small_m<kBwd>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
+    else if (lpr == 2) launch_small_m<kTrain, false, 2>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
     else launch_small_m<kTrain>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
     RM_HIP(ctx, hipGetLastError());
     if (has_bwd && !sa.final_in_kernel && (rc = reduce_and_finalize(ctx, c, a, nb, first)) != RM_OK) return rc;
@@ -4029,8 +4084,9 @@ int rm_train_iteration(rm_context* ctx, const float* ray_org, const float* ray_d
   c.loss_sum = loss_sum;
   c.accumulate = 0;
   // one launch: the small kernel with its in-kernel final reduction (RM_FUSED_ITER=0: three calls)
-  const bool fused = use_small(c, M, n) && (n + kBlock - 1) / kBlock <= kSmallFinalMaxBlocks &&
-                     (n + kBlock - 1) / kBlock <= max_blocks_per_launch() &&
+  const int rpb = kBlock / small_lpr(c, n);
+  const bool fused = use_small(c, M, n) && (n + rpb - 1) / rpb <= kSmallFinalMaxBlocks &&
+                     (n + rpb - 1) / rpb <= max_blocks_per_launch() &&
                      M <= kOptSmallMaxM && !env_is("RM_SMALL_FINAL", '0') &&
                      !env_is("RM_FUSED_ITER", '0');
   if (fused) {

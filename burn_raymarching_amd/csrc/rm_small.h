@@ -33,6 +33,7 @@ struct SmallArgs {
   FinalArgs fin;          // where the last block writes the gradients and the loss
   unsigned* arrivals;     // arrival counter (zero between launches; the last block resets it)
   int final_in_kernel;    // 1: the last block reduces and finalizes; 0: partial records only
+  int acquire;            // 1: the last block runs an agent-scope acquire before its loads
   // The fused training iteration (rm_train_iteration; kernel template FUSED): the batch is drawn
   // and gathered in the kernel (rm_sample_kernel's rows: ray i of the call reads row j of the
   // dataset arrays) and the last block runs the optimizer step on the gradient it has summed.
@@ -84,12 +85,49 @@ __device__ __forceinline__ float small_softmin(const float p[3], const SmallSphe
   return -(flog2(fmaxf(s, 1e-8f)) + m) * inv_kappa;
 }
 
-template <int MODE, int MB, bool FUSED = false>
+// The two lanes of a ray (LPR = 2) exchange their halves with one DPP move (quad_perm 1,0,3,2).
+__device__ __forceinline__ float lane_xor1(float x) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, true));
+}
+
+// small_softmin over half of the spheres in each of the two lanes of a ray (LPR = 2): the exact
+// maximum of both halves (max is exact), each lane's shifted sum, the two sums added
+// (commutative: both lanes get the same bits) -- the march's D, identical in the two lanes.
+template <int MBH>
+__device__ __forceinline__ float small_softmin_half(const float p[3], const SmallSpheres<MBH>& S, float kappa,
+                                                    float inv_kappa) {
+  const f2 PX = sp(p[0]), PY = sp(p[1]), PZ = sp(p[2]), PP = sp(psq(p)), NK = sp(-kappa);
+  f2 v[MBH / 2];
+  float m = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < MBH / 2; ++i) {
+    const f2 q = clamp_q(fma2(PZ, S.gz[i], fma2(PY, S.gy[i], fma2(PX, S.gx[i], PP + S.cc[i]))));
+    v[i] = fma2(sqrt2(q), NK, S.kr[i]);
+    m = fmaxf(m, fmaxf(v[i].x, v[i].y));
+  }
+  m = fmaxf(m, lane_xor1(m));
+  const f2 MN = sp(m);
+  f2 acc = sp(0.0f);
+#pragma unroll
+  for (int i = 0; i < MBH / 2; ++i) acc += exp2v(v[i] - MN);
+  const float sl = acc.x + acc.y;
+  const float s = sl + lane_xor1(sl);
+  return -(flog2(fmaxf(s, 1e-8f)) + m) * inv_kappa;
+}
+
+// LPR (lanes per ray, train steps): 2 -- the S march steps run with each ray's spheres split over
+// two lanes (128 rays per block, twice the waves: the reference loop's 16,384-ray batch fills
+// half of the SIMDs instead of a quarter), then the rays go through LDS to waves 0-1, which run
+// the post-march forward and the backward with one ray per lane as for LPR = 1.
+template <int MODE, int MB, bool FUSED = false, int LPR = 1>
 __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, const SmallArgs sa) {
   static_assert(MB % 2 == 0 && MB <= kSmallMaxM, "sphere bucket");
   static_assert(!FUSED || MODE == kTrain, "the fused iteration is a train step");
+  static_assert(LPR == 1 || (LPR == 2 && MODE == kTrain && MB % 4 == 0), "split march: train steps");
   constexpr int kRec = kSmallMaxM * 8 + 8;  // per-wave slot of the cross-wave sums
   constexpr int NP = MB / 2;
+  constexpr int RPB = kBlock / LPR;         // rays per block
+  constexpr int kPostWaves = kWaves / LPR;  // waves of the post-march phases
   __shared__ float4 s_geo[MB];              // {gx, gy, gz, cc}
   __shared__ float4 s_mat[MB];              // {kr, r, 0, 0}
   __shared__ float4 s_col[MB];              // {red, green, blue, 0}
@@ -98,6 +136,11 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int M = a.M;
   const float kappa = a.k * kLog2e, inv_kappa = 1.0f / kappa;
+  // measurement build (-DRM_BLOCK_TRACE): per wave, the s_memrealtime stamps of the phases
+  // (0 start, 1 end, 4 sphere data + ray, 5 march, 6 post-march forward, 7 backward sweeps,
+  // 8 record + arrival, 9 final reduction, 10 optimizer; 3 = block; tools/small_trace.py)
+  RM_TRACE(0, __builtin_amdgcn_s_memrealtime());
+  RM_TRACE(3, (unsigned long long)blockIdx.x);
 
   // ---- sphere data of the activated scene (scene.rs:41-45 values), padding spheres far away
   if (tid < MB) {
@@ -119,8 +162,8 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
 
   // ---- the ray (camera.rs:58-87 in camera mode)
   const long long blk = blockIdx.x;
-  const long long li = blk * kBlock + tid;
-  const bool valid = li < a.n_rays;
+  long long li = blk * RPB + tid / LPR;
+  bool valid = li < a.n_rays;
   long long ri = a.ray_begin + (valid ? li : 0);
   float o[3], d[3];
   int view;
@@ -141,29 +184,75 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
     ti = ri;
   }
   __syncthreads();
-  SmallSpheres<MB> S;
+  auto load_spheres = [&](auto& S, int first) {  // pairs of spheres first, first + 1, ... from LDS
+    constexpr int n = sizeof(S.gx) / sizeof(S.gx[0]);
 #pragma unroll
-  for (int i = 0; i < NP; ++i) {
-    const float4 g0 = s_geo[2 * i], g1 = s_geo[2 * i + 1];
-    S.gx[i] = f2{g0.x, g1.x};
-    S.gy[i] = f2{g0.y, g1.y};
-    S.gz[i] = f2{g0.z, g1.z};
-    S.cc[i] = f2{g0.w, g1.w};
-    S.kr[i] = f2{s_mat[2 * i].x, s_mat[2 * i + 1].x};
-  }
+    for (int i = 0; i < n; ++i) {
+      const float4 g0 = s_geo[first + 2 * i], g1 = s_geo[first + 2 * i + 1];
+      S.gx[i] = f2{g0.x, g1.x};
+      S.gy[i] = f2{g0.y, g1.y};
+      S.gz[i] = f2{g0.z, g1.z};
+      S.cc[i] = f2{g0.w, g1.w};
+      S.kr[i] = f2{s_mat[first + 2 * i].x, s_mat[first + 2 * i + 1].x};
+    }
+  };
 
+  RM_TRACE(4, __builtin_amdgcn_s_memrealtime());
   // ---- march: t <- (t + sdf(o + d t)).detach(), S times (renderer_diff.rs:20-26)
   float t = 0.0f;
-  if (MODE == kBwd && a.t_in != nullptr) {
-    t = a.t_in[ri];
-  } else {
+  if constexpr (LPR == 2) {
+    SmallSpheres<MB / 2> SH;  // this lane's half: spheres (tid & 1) * MB / 2 ...
+    load_spheres(SH, (tid & 1) * (MB / 2));
     for (int st = 0; st < a.steps; ++st) {
       const float p[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
-      float m, s;
-      t = fminf(t + small_softmin<MB, false>(p, S, kappa, inv_kappa, m, s), kTMax);
+      t = fminf(t + small_softmin_half<MB / 2>(p, SH, kappa, inv_kappa), kTMax);
+    }
+    // the rays to waves 0-1, one per lane: origin, direction, t, rows
+    __shared__ float s_rf[8][RPB];
+    __shared__ long long s_rr[2][RPB];
+    const int rl = tid >> 1;
+    if ((tid & 1) == 0) {
+      s_rf[0][rl] = o[0];
+      s_rf[1][rl] = o[1];
+      s_rf[2][rl] = o[2];
+      s_rf[3][rl] = d[0];
+      s_rf[4][rl] = d[1];
+      s_rf[5][rl] = d[2];
+      s_rf[6][rl] = t;
+      s_rr[0][rl] = ri;
+      s_rr[1][rl] = ti;
+    }
+    __syncthreads();
+    // waves 0-1: ray tid of the block; waves 2-3 repeat the rays of waves 0-1 as invalid rays
+    // (no outputs, zero seeds, their sums not added: block_sum takes waves 0-1), so that every
+    // loop and barrier below keeps the full block
+    const int r2 = tid % RPB;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      o[c] = s_rf[c][r2];
+      d[c] = s_rf[3 + c][r2];
+    }
+    t = s_rf[6][r2];
+    ri = s_rr[0][r2];
+    ti = s_rr[1][r2];
+    li = blk * RPB + r2;
+    valid = li < a.n_rays && wave < kPostWaves;
+  }
+  SmallSpheres<MB> S;
+  load_spheres(S, 0);
+  if constexpr (LPR == 1) {
+    if (MODE == kBwd && a.t_in != nullptr) {
+      t = a.t_in[ri];
+    } else {
+      for (int st = 0; st < a.steps; ++st) {
+        const float p[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
+        float m, s;
+        t = fminf(t + small_softmin<MB, false>(p, S, kappa, inv_kappa, m, s), kTMax);
+      }
     }
   }
   if (MODE == kFwd && a.t_out != nullptr && valid) a.t_out[ri] = t;
+  RM_TRACE(5, __builtin_amdgcn_s_memrealtime());
 
   // ---- reconnect: t_final = t + sdf(p_approx) (renderer_diff.rs:30-39)
   const float pa[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
@@ -231,6 +320,7 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
     a.out[3 * ri + 1] = outv[1];
     a.out[3 * ri + 2] = outv[2];
   }
+  RM_TRACE(6, __builtin_amdgcn_s_memrealtime());
   if constexpr (MODE == kFwd) return;
 
   // ---- seed g = dL/dout (training.rs:17-34 in the train step)
@@ -318,6 +408,7 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
       red[(2 * i + 1) * 8 + (lane >> 3)] = rb0;
     }
   }
+  RM_TRACE(7, __builtin_amdgcn_s_memrealtime());
   __syncthreads();
 
   // ---- the block's partial record [Mpad][8] | 8 scalars (the rm_reduce_partials layout), the
@@ -335,7 +426,7 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
     if (!zero) {
       v = s_red[src];
 #pragma unroll
-      for (int w = 1; w < kWaves; ++w) v += s_red[w * kRec + src];
+      for (int w = 1; w < kPostWaves; ++w) v += s_red[w * kRec + src];
     }
     return e == ncols - 1 ? 1.0f : v;  // scalar 7: live flag (rm_reduce_partials reads every column)
   };
@@ -360,30 +451,45 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
     s_last = prev == gridDim.x - 1 ? 1 : 0;
   }
   __syncthreads();
+  RM_TRACE(8, __builtin_amdgcn_s_memrealtime());
+  RM_TRACE(1, __builtin_amdgcn_s_memrealtime());
   if (!s_last) return;
-  if (tid == 0) {
+  // FUSED: the optimizer's parameters and moments load while the block sums the records
+  OptPrefetch pf;
+  if constexpr (FUSED) pf = opt_prefetch(sa.raw, sa.m1, sa.m2, M);
+  // The records are read with write-through-cache (sc1) loads only, stored sc1 by every block,
+  // each storing wave drained (vmcnt(0)) before the barrier behind which one lane adds to the one
+  // counter whose last add tells this block: the hand-off row of MI355X_MICROARCH.md
+  // (inter-workgroup visibility) under which sc1 loads may replace the agent-scope acquire. The
+  // acquire is kept (sa.acquire, env RM_SMALL_ACQUIRE=0 drops it): without it the tail measured
+  // the same (tools/small_trace.py: 4.96 vs 5.12 us at 128 blocks).
+  if (sa.acquire && tid == 0) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  // each needed column is summed by `chains` threads (rows b = k mod chains, in order, eight in
-  // flight), the chains then added in order: a fixed order for every launch of this size
+  // each needed column is summed by `chains` threads (rows b = k mod chains, in order), the chains
+  // then added in order: a fixed order for every launch of this size. The write-through loads
+  // miss the local L2 (~1 us each round trip): kFinBatch rows in flight per thread, so that a
+  // launch of up to kSmallFinalMaxBlocks blocks takes one or two rounds.
+  constexpr int kFinBatch = 32;
   const int nb = gridDim.x;
   const int chains = max(1, min(8, kBlock / nneed));
   for (int w = tid; w < nneed * chains; w += kBlock) {
     const int idx = w % nneed, ch = w / nneed;
     const long long e = col_of(idx);
     float acc = 0.0f;
-    for (int b0 = ch; b0 < nb; b0 += 8 * chains) {
-      float v[8];
+    for (int b0 = ch; b0 < nb; b0 += kFinBatch * chains) {
+      float v[kFinBatch];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < kFinBatch; ++u) {
         const int b = b0 + u * chains;
-        v[u] = __hip_atomic_load(a.partials + (long long)min(b, nb - 1) * a.rec + e, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+        v[u] = b < nb ? __hip_atomic_load(a.partials + (long long)b * a.rec + e, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT)
+                      : 0.0f;
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
+      for (int u = 0; u < kFinBatch; ++u)
         if (b0 + u * chains < nb) acc += v[u];
     }
     s_red[ch * nneed + idx] = acc;
@@ -395,6 +501,12 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
     for (int ch = 1; ch < chains; ++ch) v += s_red[ch * nneed + idx];
     return v;
   };
+  // FUSED: the gradient also goes to LDS in the packed layout the optimizer reads
+  [[maybe_unused]] float* s_gact = nullptr;
+  if constexpr (FUSED) {
+    __shared__ float s_gact_buf[7 * kSmallMaxM + 4];
+    s_gact = s_gact_buf;
+  }
   for (int idx = tid; idx < M * 8; idx += kBlock) {
     const int j = idx >> 3, comp = idx & 7;
     if (comp == 7) continue;
@@ -402,6 +514,7 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
                           : (comp == 3 ? (f.gr ? f.gr + j : nullptr) : (f.gcol ? f.gcol + 3 * j + (comp - 4) : nullptr));
     const float v = total(idx);
     if (dst) *dst = f.accumulate ? *dst + v : v;
+    if constexpr (FUSED) s_gact[comp < 3 ? 3 * j + comp : (comp == 3 ? 6 * M + j : 3 * M + 3 * j + (comp - 4))] = v;
   }
   if (tid == 0) {
     const float sc[5] = {total(M * 8), total(M * 8 + 1), total(M * 8 + 2), total(M * 8 + 3), total(M * 8 + 4)};
@@ -414,19 +527,24 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
       for (int c = 0; c < 3; ++c) {
         const float gv = (sc[c] - ln[c] * proj) / len;
         f.gld[c] = f.accumulate ? f.gld[c] + gv : gv;
+        if constexpr (FUSED) s_gact[7 * M + c] = gv;
       }
     }
+    if constexpr (FUSED) s_gact[7 * M + 3] = sc[3];
     if (f.gamb) f.gamb[0] = f.accumulate ? f.gamb[0] + sc[3] : sc[3];
     if (f.loss_sum) f.loss_sum[0] = f.accumulate ? f.loss_sum[0] + sc[4] : sc[4];
     __hip_atomic_store(sa.arrivals, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
   }
+  RM_TRACE(9, __builtin_amdgcn_s_memrealtime());
+  RM_TRACE(1, __builtin_amdgcn_s_memrealtime());
   if constexpr (FUSED) {
     // the optimizer step (rm_optimizer_step: penalties + Adam, train.rs:198) on the gradient just
-    // written -- from this block's own stores (visible to the block after the barrier), in the
-    // packed layout the optimizer reads. Every other block has arrived, so nothing reads the
-    // activated parameters any more when act_out overwrites them.
+    // summed (its LDS copy in the packed layout). Every other block has arrived, so nothing reads
+    // the activated parameters any more when act_out overwrites them.
     __syncthreads();
-    optimizer_small_block(sa.raw, f.gc, sa.m1, sa.m2, M, sa.step, sa.lr, sa.wd, sa.with_pen, sa.loss_penalty,
+    optimizer_small_block(pf, sa.raw, s_gact, sa.m1, sa.m2, M, sa.step, sa.lr, sa.wd, sa.with_pen, sa.loss_penalty,
                           sa.act_out, nullptr);
+    RM_TRACE(10, __builtin_amdgcn_s_memrealtime());
+    RM_TRACE(1, __builtin_amdgcn_s_memrealtime());
   }
 }
