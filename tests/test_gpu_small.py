@@ -78,6 +78,26 @@ def test_reference_training_call(rm, oracle, monkeypatch, m, k):
     check_grads(g, g_ref, mode="train")
 
 
+@pytest.mark.parametrize("lpr", ["1", "2"])
+@pytest.mark.parametrize("m", [4, 9, 32])
+def test_lanes_per_ray(rm, oracle, monkeypatch, m, lpr):
+    """Train steps with one lane per ray and with the march split over two lanes (RM_SMALL_LPR,
+    the default for <= 32,768 rays): both against the oracle, and within fp32 rounding of each other."""
+    render, model, _ = rm
+    monkeypatch.setenv("RM_SMALL_LPR", lpr)
+    n, steps = 16384, 40
+    sc = train_scene(model, m, 60 + m)
+    o, d = batch(oracle, model, n, 100 + m)
+    o64, d64 = o.astype(np.float64), d.astype(np.float64)
+    targets = oracle.render_diff(o64, d64, train_scene(model, 5, 8), steps, 32.0)
+    out_ref, loss_ref, g_ref = oracle.train_step(o64, d64, targets, sc, steps, 24.0, 0.6)
+    loss, g, out = render.train_step(dev(o), dev(d), dev(targets), model.scene_tensors(sc), 24.0, 0.6, steps,
+                                     with_out=True)
+    check_fwd(host(out), out_ref)
+    assert abs(host(loss)[0] - loss_ref) <= 1e-4 * abs(loss_ref) + 1e-3
+    check_grads(g, g_ref, mode="train")
+
+
 @pytest.mark.parametrize("m", [1, 4, 8, 12, 16, 17, 24, 32])
 @pytest.mark.parametrize("n", [1, 257, 4096])
 def test_bucket_edges_forward_backward(rm, oracle, m, n):
