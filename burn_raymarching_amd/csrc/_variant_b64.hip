@@ -38,7 +38,7 @@
 #include <vector>
 
 #include "../../include/raymarch.h"
-#include "rm_device.h"
+#include "_variant_device_b64.h"
 
 #ifndef RM_PRIO_RAMP
 // s_setprio ramp over the march / post-march / backward phases: paid off when one launch filled
@@ -2935,7 +2935,7 @@ int fail(rm_context* ctx, int code, const char* fmt, ...) {
 
 // Centre-out dispatch order of the ray blocks of a view's tx x ty 16x16 tiles (ray_block): by
 // distance of the block's pixel-centre from the image centre, ties by block index. A block is a
-// whole tile (256-ray blocks) or one of its four 8x8 quadrants (64-ray blocks: the split march), in
+// whole tile (256-ray blocks) or one of its four 8x8 quadrants (64-ray blocks, RM_BLOCK=64), in
 // the pixel order of setup_ray. Built once per image size.
 int ensure_block_order(rm_context* ctx, int tx, int ty, int sub) {
   if (ctx->block_order && ctx->order_tx == tx && ctx->order_ty == ty && ctx->order_sub == sub) return RM_OK;
