@@ -64,7 +64,7 @@ PEAK_HBM_GBS = 8000.0      # MI355X_MICROARCH.md chip table (spec)
 FLOP_PER_EVAL = 16         # SURVEY.md §8d canonical count (sqrt and exp counted as 1)
 BYTES_PER_RAY_CAMERA = 24  # SURVEY.md §8d algorithmic HBM bytes per ray, camera mode
 DEFAULT_GLOBAL_VIEWS = 80  # strong scaling: 80 views per step = 10 per GPU at N = 8
-MAX_RAYS_PER_CALL = 16 * 512 * 512  # one launch of 256-ray blocks (kMaxBlocksPerLaunch)
+MAX_RAYS_PER_CALL = 128 * 512 * 512  # one launch of 256-ray blocks (kMaxBlocksPerLaunch)
 
 
 def parse():
@@ -85,7 +85,8 @@ def parse():
                          "configs[1-2] = 2,621,440 rays in one launch); exclusive with --global-views")
     ap.add_argument("--ring", type=int, default=10, help="cameras on the target ring (at least the views of a step)")
     ap.add_argument("--views-per-call", type=int, default=0,
-                    help="views per train call (0: as many as one launch takes, up to 16)")
+                    help="views per train call (0: as many as one launch takes, up to 128 = the strong default's "
+                         "80 views in one call)")
     ap.add_argument("--streams", type=int, default=1,
                     help="HIP streams the calls of a step are spread over (>1: the calls run concurrently, each "
                          "into its own gradient row, summed in call order before the all-reduce)")
@@ -214,13 +215,13 @@ def main():
     W, H, M, S, K = args.width, args.height, args.spheres, args.march_steps, args.smooth_k
     strong = args.global_views is not None
     if not strong and not 1 <= args.views_per_gpu <= native.RM_MAX_VIEWS_PER_CALL:
-        raise SystemExit("--views-per-gpu must be in 1..16")
+        raise SystemExit(f"--views-per-gpu must be in 1..{native.RM_MAX_VIEWS_PER_CALL}")
     npix = W * H
     shard = Shard(rank, world, 0 if strong else args.views_per_gpu, 1, args.global_views or 0)
     vpg = shard.count()  # this rank's views per step
     rays_per_rank = vpg * npix
     rays_global = shard.views_total * npix
-    # views per train call (one launch of up to 16 views / 4M rays each)
+    # views per train call (one launch of up to 128 views / 33.5M rays each)
     views_per_call = max(1, min(native.RM_MAX_VIEWS_PER_CALL, MAX_RAYS_PER_CALL // npix))
     if args.views_per_call > 0:
         views_per_call = min(views_per_call, args.views_per_call)

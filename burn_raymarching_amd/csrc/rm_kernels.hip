@@ -79,7 +79,11 @@ namespace rm {
 enum Mode { kFwd = 0, kBwd = 1, kTrain = 2, kRender = 3 };
 
 // bounds the partial-gradient workspace per launch: 16 views of 512x512
-constexpr int kMaxBlocksPerLaunch = 16384 * (256 / kBlock);
+// 128 views of 512 x 512 in one launch (per-launch ramp-down and the per-call record, origin
+// and reduction launches amortised over all the views of a step)
+constexpr int kMaxBlocksPerLaunch = 131072 * (256 / kBlock);
+// camera bases carried in the kernel arguments; calls with more views read a device table
+constexpr int kInlineCams = 16;
 // automatic split march (RM_MARCH_SPLIT): from kSplitMinSpheres spheres for launches of at most
 // kSplitMaxRays rays (about one fill of the GPU: 1024 resident 256-ray blocks), from
 // kSplitMinSpheresWide for launches of at most kSplitMaxRaysWide (four fills) -- measured
@@ -130,7 +134,8 @@ struct KArgs {
   int* olist_w;
   int* ocnt_w;
   int* ocnt_z;
-  CamBasis cams[RM_MAX_VIEWS_PER_CALL];
+  CamBasis cams[kInlineCams];  // views <= kInlineCams
+  const CamBasis* cams_dev;    // more views: the bases in device memory (cams unused), else NULL
   // activated scene
   const float* centers;
   const float* colors;
@@ -849,7 +854,8 @@ __device__ void write_origins(const KArgs& a, const float4& S00, const float4& S
     Wq += (size_t)r0 * 32;
   }
   {
-    const float p[3] = {a.cams[v].eye[0], a.cams[v].eye[1], a.cams[v].eye[2]};
+    const CamBasis& cb = a.cams_dev != nullptr ? a.cams_dev[v] : a.cams[v];
+    const float p[3] = {cb.eye[0], cb.eye[1], cb.eye[2]};
     float D = __builtin_nanf("");
     // the first step's choice in soft_min_march: unshifted when sphere 0 proves it safe, else
     // the fixed shift (else the vector path: not shared); block-uniform
@@ -1229,7 +1235,8 @@ __device__ __forceinline__ void setup_ray(const KArgs& a, long long& ri, float o
       x = (int)(pix - (long long)y * a.width);
     }
     ri = (long long)v * npix + (long long)y * a.width + x;
-    camera_ray(a.cams[v], x, y, a.width, a.height, o, d);
+    if (a.cams_dev != nullptr) camera_ray(a.cams_dev[v], x, y, a.width, a.height, o, d);
+    else camera_ray(a.cams[v], x, y, a.width, a.height, o, d);
   } else {
     o[0] = a.org[3 * ri];
     o[1] = a.org[3 * ri + 1];
@@ -2375,7 +2382,14 @@ constexpr int kReduceBatch = RM_REDUCE_BATCH;  // partial rows in flight per thr
 #endif
 static_assert((kReduceSegs / 4) % RM_FIN_U == 0, "finalize_block rounds");
 
-__device__ void finalize_block(const float* S, int M, int Mpad, const FinalArgs& f, float* tot);
+__device__ void finalize_block(const float* S, int nseg, int M, int Mpad, const FinalArgs& f, float* tot);
+
+// Segments of the reduction of nblocks ray blocks: kReduceSegs, or as many multiples of 64 as a
+// launch of more than kReduceSegs * 256 blocks needs (a segment's rows fit pass 1's 256-entry list)
+__host__ __device__ inline int reduce_segs(long long nblocks) {
+  const long long need = (nblocks + 255) / 256;
+  return need <= kReduceSegs ? kReduceSegs : (int)((need + 63) / 64 * 64);
+}
 
 __global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restrict__ P, long long rec, int M, int Mpad,
                                                           int nblocks, int seg_len, float* __restrict__ S,
@@ -2435,14 +2449,14 @@ __global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restric
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
-  finalize_block(S, M, Mpad, f, tot);
+  finalize_block(S, (int)gridDim.y, M, Mpad, f, tot);
   if (tid == 0) __hip_atomic_store(arrivals + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Pass 2 for the 256 columns of pass-1 column block blockIdx.x, by the block of that column block
 // that arrived last: thread t sums column t's kReduceSegs segments in the four chains s mod 4 of
 // rm_finalize_grads, combined (a0 + a1) + (a2 + a3) -- the same bits -- then the scatter.
-__device__ void finalize_block(const float* S, int M, int Mpad, const FinalArgs& f, float* tot) {
+__device__ void finalize_block(const float* S, int nseg, int M, int Mpad, const FinalArgs& f, float* tot) {
   const int ncols = Mpad * 8 + 8;
   const int tid = threadIdx.x;
   const int col = blockIdx.x * 256 + tid;
@@ -2450,7 +2464,7 @@ __device__ void finalize_block(const float* S, int M, int Mpad, const FinalArgs&
   // kU * 4 loads in flight per thread (the last block runs alone: registers are free)
   constexpr int kU = RM_FIN_U;
   float a[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  for (int u0 = 0; u0 < kReduceSegs / 4; u0 += kU) {
+  for (int u0 = 0; u0 < nseg / 4; u0 += kU) {
     float v[kU][4];
 #pragma unroll
     for (int u = 0; u < kU; ++u)
@@ -2508,16 +2522,21 @@ __global__ __launch_bounds__(256) void rm_finalize_grads(const float* __restrict
   const int ncols = Mpad * 8 + 8;
   const int cl = threadIdx.x & 63, chain = threadIdx.x >> 6;
   const int col = blockIdx.x * 64 + cl;
-  (void)nseg;  // == kReduceSegs always (pass 1 writes every segment, empty ones as 0)
   static_assert(kReduceSegs % 64 == 0, "four chains of 16-load rounds");
   {
-    float v[kReduceSegs / 4];
+    // nseg (reduce_segs: a multiple of 64) segments, chain `chain` sums s = chain mod 4 in order,
+    // kReduceSegs / 4 loads in flight
+    constexpr int kC = kReduceSegs / 4;
     const int c = min(col, ncols - 1);
-#pragma unroll
-    for (int u = 0; u < kReduceSegs / 4; ++u) v[u] = S[(long long)(4 * u + chain) * ncols + c];
     float acc = 0.0f;
+    for (int u0 = 0; u0 < nseg / 4; u0 += kC) {
+      float v[kC];
 #pragma unroll
-    for (int u = 0; u < kReduceSegs / 4; ++u) acc += v[u];
+      for (int u = 0; u < kC; ++u) v[u] = u0 + u < nseg / 4 ? S[(long long)(4 * (u0 + u) + chain) * ncols + c] : 0.0f;
+#pragma unroll
+      for (int u = 0; u < kC; ++u)
+        if (u0 + u < nseg / 4) acc += v[u];
+    }
     part[chain][cl] = acc;
   }
   __syncthreads();
@@ -2892,6 +2911,10 @@ struct rm_context {
   void* rec = nullptr;                      // sphere records of the current call (rm_prep_kernel)
   unsigned* arrivals = nullptr;             // rm_small_kernel's arrival counter (zero between launches)
   unsigned* red_arrivals = nullptr;         // rm_reduce_partials' per-column-block arrival counters
+  rm::CamBasis* cams_dev = nullptr;         // camera bases of calls with > kInlineCams views (device)
+  rm::CamBasis* cams_pin = nullptr;         // their pinned host staging, kCamRing slots
+  hipEvent_t cam_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // slot k's copy has been issued
+  int cam_slot = 0;
   float* batch = nullptr;                   // rm_train_iteration's unfused path: the drawn batch (9 floats/ray)
   size_t batch_bytes = 0;
   size_t rec_bytes = 0;
@@ -3008,7 +3031,7 @@ size_t ws_need(long long max_rays, int M, int rays_per_block = kBlock) {
   long long blocks = (max_rays + rays_per_block - 1) / rays_per_block;
   blocks = std::min<long long>(blocks, kMaxBlocksPerLaunch);
   const long long rec = rec_floats(Mpad);
-  return (size_t)(blocks * rec + (long long)kReduceSegs * rec + 4096) * sizeof(float);
+  return (size_t)(blocks * rec + (long long)reduce_segs(blocks) * rec + 4096) * sizeof(float);
 }
 
 int ensure_ws(rm_context* ctx, size_t bytes) {
@@ -3126,10 +3149,9 @@ int reduce_and_finalize(rm_context* ctx, const Call& c, const KArgs& a, long lon
   const int nblocks = (int)nb;
   const int ncols = a.Mpad * 8 + 8;
   float* S = a.partials + (long long)std::max<long long>(nb, 1) * a.rec;
-  const int segs = kReduceSegs;  // every segment is written (empty ones as 0)
+  const int segs = reduce_segs(nblocks);  // every segment is written (empty ones as 0)
   const int seg_len = (nblocks + segs - 1) / segs;
   // pass 1 compacts a segment's rows in one 256-entry list (rm_reduce_partials)
-  static_assert(kMaxBlocksPerLaunch <= kReduceSegs * 256, "a segment holds at most 256 ray blocks");
   if (seg_len > 256) return fail(ctx, RM_ERR_INVALID_ARG, "%d ray blocks in one launch", nblocks);
   const int xblocks = (ncols + 255) / 256;
   // pass 2 in the same launch (the last-arriving segment block of each column block) unless
@@ -3291,6 +3313,32 @@ void launch_ray(bool cam, bool split, dim3 grid, size_t lds, hipStream_t st, con
   }
 }
 
+// Camera bases of a call with more than kInlineCams views: built on the host (make_basis), staged
+// in one of kCamRing pinned slots and copied to the context's device table on its stream (the
+// copy is ordered after the previous call's kernels, so one device table serves every call; a
+// pinned slot is rewritten only after its previous copy has run).
+constexpr int kCamRing = 4;
+int upload_cams(rm_context* ctx, const Call& c, KArgs& a) {
+  int rc;
+  if (!ctx->cams_dev) {
+    if (hipMalloc(&ctx->cams_dev, sizeof(CamBasis) * RM_MAX_VIEWS_PER_CALL) != hipSuccess)
+      return fail(ctx, RM_ERR_OOM, "camera table");
+    if (hipHostMalloc(&ctx->cams_pin, sizeof(CamBasis) * RM_MAX_VIEWS_PER_CALL * kCamRing) != hipSuccess)
+      return fail(ctx, RM_ERR_OOM, "camera staging");
+    for (hipEvent_t& e : ctx->cam_ev) RM_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  const int slot = ctx->cam_slot;
+  ctx->cam_slot = (slot + 1) % kCamRing;
+  RM_HIP(ctx, hipEventSynchronize(ctx->cam_ev[slot]));
+  CamBasis* pin = ctx->cams_pin + (size_t)slot * RM_MAX_VIEWS_PER_CALL;
+  for (int v = 0; v < c.views; ++v)
+    if ((rc = make_basis(ctx, c.cams[v], c.W, c.H, pin[v])) != RM_OK) return rc;
+  RM_HIP(ctx, hipMemcpyAsync(ctx->cams_dev, pin, sizeof(CamBasis) * c.views, hipMemcpyHostToDevice, ctx->stream));
+  RM_HIP(ctx, hipEventRecord(ctx->cam_ev[slot], ctx->stream));
+  a.cams_dev = ctx->cams_dev;
+  return RM_OK;
+}
+
 int run(rm_context* ctx, const Call& c) {
   if (!ctx) return RM_ERR_INVALID_ARG;
   int rc;
@@ -3304,8 +3352,13 @@ int run(rm_context* ctx, const Call& c) {
       return fail(ctx, RM_ERR_INVALID_ARG, "num_views %d out of [1, %d]", c.views, RM_MAX_VIEWS_PER_CALL);
     if (c.W < 1 || c.H < 1 || (long long)c.W * c.H > (1LL << 28))
       return fail(ctx, RM_ERR_INVALID_ARG, "bad image size %dx%d", c.W, c.H);
-    for (int v = 0; v < c.views; ++v)
-      if ((rc = make_basis(ctx, c.cams[v], c.W, c.H, a.cams[v])) != RM_OK) return rc;
+    a.cams_dev = nullptr;
+    if (c.views <= kInlineCams) {
+      for (int v = 0; v < c.views; ++v)
+        if ((rc = make_basis(ctx, c.cams[v], c.W, c.H, a.cams[v])) != RM_OK) return rc;
+    } else if ((rc = upload_cams(ctx, c, a)) != RM_OK) {
+      return rc;
+    }
     a.width = c.W;
     a.height = c.H;
     // Compact 16x16 tiles per block (8x8 per wave): more waves whose rays all miss the scene
@@ -3717,11 +3770,15 @@ void rm_destroy(rm_context* ctx) {
     if (ctx->ocnt) (void)hipFree(ctx->ocnt);
     if (ctx->rec) (void)hipFree(ctx->rec);
   }
-  if (ctx->arrivals || ctx->red_arrivals || ctx->batch) {
+  if (ctx->arrivals || ctx->red_arrivals || ctx->batch || ctx->cams_dev) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->arrivals) (void)hipFree(ctx->arrivals);
     if (ctx->red_arrivals) (void)hipFree(ctx->red_arrivals);
     if (ctx->batch) (void)hipFree(ctx->batch);
+    if (ctx->cams_dev) (void)hipFree(ctx->cams_dev);
+    if (ctx->cams_pin) (void)hipHostFree(ctx->cams_pin);
+    for (hipEvent_t& e : ctx->cam_ev)
+      if (e) (void)hipEventDestroy(e);
   }
   for (auto& pr : ctx->events) {
     (void)hipEventDestroy(pr.first);

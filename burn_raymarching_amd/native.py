@@ -14,7 +14,7 @@ _PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("RM_LIB_PATH") or os.path.join(_PKG, "lib", "libraymarch_hip.so")
 
 RM_OK = 0
-RM_MAX_VIEWS_PER_CALL = 16
+RM_MAX_VIEWS_PER_CALL = 128
 _ERR_NAMES = {1: "RM_ERR_INVALID_ARG", 2: "RM_ERR_HIP", 3: "RM_ERR_OOM", 4: "RM_ERR_UNSUPPORTED"}
 
 _P = ctypes.c_void_p

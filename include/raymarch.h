@@ -44,7 +44,7 @@ extern "C" {
 #define RM_ERR_UNSUPPORTED 4
 
 /* Limits of this build. */
-#define RM_MAX_VIEWS_PER_CALL 16     /* camera descriptors per rm_*_camera call */
+#define RM_MAX_VIEWS_PER_CALL 128    /* camera descriptors per rm_*_camera call */
 #define RM_MAX_SPHERES 65536
 
 typedef struct rm_context rm_context;

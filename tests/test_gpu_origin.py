@@ -89,13 +89,14 @@ def test_stats_count_shared_steps(mods, monkeypatch):
     assert s0["steps_saved"] < s1["steps_saved"] <= s0["steps_saved"] + s1["waves"]
 
 
-@pytest.mark.parametrize("views,m", [(16, 256), (5, 512), (1, 8)])
+@pytest.mark.parametrize("views,m", [(16, 256), (5, 512), (1, 8), (40, 64), (128, 40)])
 def test_origins_up_to_16_views(mods, monkeypatch, views, m):
-    """Per-view origin steps for up to 16 views per call (one wave per view in rm_origin_kernel):
-    images, loss and gradients equal (==) to the per-ray first step."""
+    """Per-view origin steps for up to 128 views per call (one wave per view in rm_origin_kernel;
+    beyond 16 views the camera bases come from the context's device table): images, loss and
+    gradients equal (==) to the per-ray first step."""
     torch, model, native, render = mods
     sc = model.scene_tensors(model.synthetic_scene(m, 6), "cuda")
-    cams = model.ring_cameras(16)[:views]
+    cams = model.ring_cameras(max(16, views))[:views]
     tgt = render.render_diff_camera(cams, 32, 32, model.scene_tensors(model.synthetic_scene(m, 9), "cuda"), 32.0, 24)
 
     def run():
@@ -110,3 +111,29 @@ def test_origins_up_to_16_views(mods, monkeypatch, views, m):
     assert torch.equal(shared[2], per_ray[2])
     for key in shared[1]:
         assert torch.equal(shared[1][key], per_ray[1][key]), key
+
+
+@pytest.mark.parametrize("views", [17, 40, 128])
+def test_many_views_per_call(mods, monkeypatch, views):
+    """A call of more than 16 views (device camera table, kInlineCams) renders what calls of at most
+    16 views render, bit for bit (per-ray outputs), and its train step's gradient equals the sum of
+    the smaller calls' to fp32 rounding (another block order in the reduction)."""
+    import numpy as np
+    torch, model, native, render = mods
+    monkeypatch.setenv("RM_SMALL", "0")
+    sc = model.scene_tensors(model.synthetic_scene(48, 3), "cuda")
+    cams = model.ring_cameras(views)
+    one = render.render_diff_camera(cams, 32, 32, sc, 32.0, 24)
+    parts = torch.cat([render.render_diff_camera(cams[i:i + 16], 32, 32, sc, 32.0, 24) for i in range(0, views, 16)])
+    assert torch.equal(one, parts)
+    tgt = render.render_diff_camera(cams, 32, 32, model.scene_tensors(model.synthetic_scene(48, 4), "cuda"), 32.0, 24)
+    n = views * 32 * 32
+    _, g1, _ = render.train_step_camera(cams, 32, 32, tgt, sc, 32.0, 0.3, 24, inv_count=1.0 / (3 * n))
+    acc = None
+    for i in range(0, views, 16):
+        _, g, _ = render.train_step_camera(cams[i:i + 16], 32, 32, tgt[i * 1024:(i + 16) * 1024], sc, 32.0, 0.3, 24,
+                                           inv_count=1.0 / (3 * n))
+        acc = {k: v.clone() for k, v in g.items()} if acc is None else {k: acc[k] + g[k] for k in g}
+    for k in g1:
+        a, b = g1[k].cpu().numpy(), acc[k].cpu().numpy()
+        assert np.abs(a - b).max() <= 1e-5 * max(np.abs(b).max(), 1e-12), k

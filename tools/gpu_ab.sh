@@ -1,7 +1,8 @@
 # Same-box A/B of variants on bench configurations, alternating A B A B over ROUNDS rounds.
 # A variant is "default", an environment assignment list ("RM_SPLIT=0 RM_SMALL=1") or
 # "lib:<name>" (the kernel library burn_raymarching_amd/lib/var/<name>.so, built with
-# tools/build_variant.sh). Configs: m (metric, strong default), m10 (10 views per GPU), ms / ms8 (the
+# tools/build_variant.sh). Configs: m (metric, strong default), m10 (10 views per GPU), m16 (the default's
+# 80 views in calls of 16), ms / ms8 (the
 # default's calls on 4 streams, 16 / 8 views per call), c2, c3,
 # c4, c5, c5r1 (C5 on a fixed view), c5s (C5 on a 64x64 view).
 #   CONFIGS="m c5" ROUNDS=2 bash tools/gpu_ab.sh default "RM_X=1" lib:trace
@@ -24,6 +25,7 @@ for r in $(seq 1 $ROUNDS); do
       case $c in
         m) args="--steps 10" ;;
         m10) args="--views-per-gpu 10 --steps 20" ;;
+        m16) args="--views-per-call 16 --steps 10" ;;
         ms) args="--streams 4 --steps 10" ;;
         ms8) args="--streams 4 --views-per-call 8 --steps 10" ;;
         c2) args="--width 256 --height 256 --spheres 64 --views-per-gpu 10 --steps 20" ;;
