@@ -2913,7 +2913,7 @@ struct rm_context {
   unsigned* red_arrivals = nullptr;         // rm_reduce_partials' per-column-block arrival counters
   rm::CamBasis* cams_dev = nullptr;         // camera bases of calls with > kInlineCams views (device)
   rm::CamBasis* cams_pin = nullptr;         // their pinned host staging, kCamRing slots
-  hipEvent_t cam_ev[4] = {nullptr, nullptr, nullptr, nullptr};  // slot k's copy has been issued
+  hipEvent_t cam_ev[32] = {};               // slot k's copy has run (kCamRing slots)
   int cam_slot = 0;
   float* batch = nullptr;                   // rm_train_iteration's unfused path: the drawn batch (9 floats/ray)
   size_t batch_bytes = 0;
@@ -3317,7 +3317,8 @@ void launch_ray(bool cam, bool split, dim3 grid, size_t lds, hipStream_t st, con
 // in one of kCamRing pinned slots and copied to the context's device table on its stream (the
 // copy is ordered after the previous call's kernels, so one device table serves every call; a
 // pinned slot is rewritten only after its previous copy has run).
-constexpr int kCamRing = 4;
+constexpr int kCamRing = 32;  // calls of > 16 views in flight before the host waits for a slot
+static_assert(sizeof(rm_context::cam_ev) / sizeof(hipEvent_t) == kCamRing, "one event per staging slot");
 int upload_cams(rm_context* ctx, const Call& c, KArgs& a) {
   int rc;
   if (!ctx->cams_dev) {
