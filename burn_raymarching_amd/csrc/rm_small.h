@@ -54,6 +54,16 @@ struct SmallArgs {
 
 // Per-sphere march data in registers, pair p = spheres (2p, 2p + 1): gx = -2c, cc = |c|^2
 // (expansion form, scene.rs:66-71), kr = kappa r (kappa = smooth_k log2 e).
+// *dst = v, or *dst += v when accumulating: the load only on the accumulate branch (a select
+// would let the compiler issue it anyway, a memory round trip on the last block's tail)
+__device__ __forceinline__ void store_or_add(float* dst, float v, int accumulate) {
+  if (accumulate) {
+    *dst += v;
+  } else {
+    *dst = v;
+  }
+}
+
 template <int MB>
 struct SmallSpheres {
   f2 gx[MB / 2], gy[MB / 2], gz[MB / 2], cc[MB / 2], kr[MB / 2];
@@ -138,7 +148,8 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
   const float kappa = a.k * kLog2e, inv_kappa = 1.0f / kappa;
   // measurement build (-DRM_BLOCK_TRACE): per wave, the s_memrealtime stamps of the phases
   // (0 start, 1 end, 4 sphere data + ray, 5 march, 6 post-march forward, 7 backward sweeps,
-  // 8 record + arrival, 9 final reduction, 10 optimizer; 3 = block; tools/small_trace.py)
+  // 8 record + arrival, 11 acquire, 2 record sums, 9 final reduction, 10 optimizer; 3 = block;
+  // tools/small_trace.py)
   RM_TRACE(0, __builtin_amdgcn_s_memrealtime());
   RM_TRACE(3, (unsigned long long)blockIdx.x);
 
@@ -468,6 +479,7 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
+  RM_TRACE(11, __builtin_amdgcn_s_memrealtime());
   // each needed column is summed by `chains` threads (rows b = k mod chains, in order), the chains
   // then added in order: a fixed order for every launch of this size. The write-through loads
   // miss the local L2 (~1 us each round trip): kFinBatch rows in flight per thread, so that a
@@ -495,6 +507,7 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
     s_red[ch * nneed + idx] = acc;
   }
   __syncthreads();
+  RM_TRACE(2, __builtin_amdgcn_s_memrealtime());
   const FinalArgs& f = sa.fin;
   auto total = [&](int idx) {
     float v = s_red[idx];
@@ -513,7 +526,7 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
     float* dst = comp < 3 ? (f.gc ? f.gc + 3 * j + comp : nullptr)
                           : (comp == 3 ? (f.gr ? f.gr + j : nullptr) : (f.gcol ? f.gcol + 3 * j + (comp - 4) : nullptr));
     const float v = total(idx);
-    if (dst) *dst = f.accumulate ? *dst + v : v;
+    if (dst) store_or_add(dst, v, f.accumulate);
     if constexpr (FUSED) s_gact[comp < 3 ? 3 * j + comp : (comp == 3 ? 6 * M + j : 3 * M + 3 * j + (comp - 4))] = v;
   }
   if (tid == 0) {
@@ -526,13 +539,13 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
         const float gv = (sc[c] - ln[c] * proj) / len;
-        f.gld[c] = f.accumulate ? f.gld[c] + gv : gv;
+        store_or_add(f.gld + c, gv, f.accumulate);
         if constexpr (FUSED) s_gact[7 * M + c] = gv;
       }
     }
     if constexpr (FUSED) s_gact[7 * M + 3] = sc[3];
-    if (f.gamb) f.gamb[0] = f.accumulate ? f.gamb[0] + sc[3] : sc[3];
-    if (f.loss_sum) f.loss_sum[0] = f.accumulate ? f.loss_sum[0] + sc[4] : sc[4];
+    if (f.gamb) store_or_add(f.gamb, sc[3], f.accumulate);
+    if (f.loss_sum) store_or_add(f.loss_sum, sc[4], f.accumulate);
     __hip_atomic_store(sa.arrivals, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
   }
   RM_TRACE(9, __builtin_amdgcn_s_memrealtime());

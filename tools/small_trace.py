@@ -87,6 +87,9 @@ def main():
     if last.any():
         t9, t10 = us(9)[last], us(10)[last]
         res["final_reduction_us"] = float((t9 - us(8)[last]).max())
+        res["final_acquire_us"] = float((us(11)[last] - us(8)[last]).max())
+        res["final_record_sums_us"] = float((us(2)[last] - us(11)[last]).max())
+        res["final_scatter_us"] = float((t9 - us(2)[last]).max())
         res["optimizer_us"] = float((t10 - t9).max()) if (tr[last, 10] != 0).any() else None
     print(json.dumps(res, indent=1))
 
