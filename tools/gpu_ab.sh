@@ -37,7 +37,15 @@ for r in $(seq 1 $ROUNDS); do
       esac
       env $envs timeout -k 10 200 python bench.py --cpu-baseline off $args > gpurun_out/ab/${c}_v${i}_$r.json \
         2> gpurun_out/ab/${c}_v${i}_$r.err || { tail -5 gpurun_out/ab/${c}_v${i}_$r.err; exit 1; }
-      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], sys.argv[3], d['value'], d['ms_per_step'], r['kernel_ms_per_step'], r['frac'], r['executed_frac'])" gpurun_out/ab/${c}_v${i}_$r.json $c "$v"
+      # a variant whose executed work differs from the first variant's did other work (e.g. trained
+      # differently): its time is not comparable, and the line says so
+      python3 -c "
+import json, sys
+d = json.load(open(sys.argv[1])); r = d['roofline']
+ref = json.load(open(sys.argv[4]))['roofline']['executed_frac']
+flag = '' if abs(r['executed_frac'] - ref) <= 1e-4 else '  WORK DIFFERS FROM VARIANT 1'
+print(sys.argv[2], sys.argv[3], d['value'], d['ms_per_step'], r['kernel_ms_per_step'], r['frac'], r['executed_frac'], flag)
+" gpurun_out/ab/${c}_v${i}_$r.json $c "$v" gpurun_out/ab/${c}_v1_$r.json
     done
   done
 done
