@@ -113,20 +113,21 @@ def test_origins_up_to_16_views(mods, monkeypatch, views, m):
         assert torch.equal(shared[1][key], per_ray[1][key]), key
 
 
-@pytest.mark.parametrize("views", [17, 40, 128])
-def test_many_views_per_call(mods, monkeypatch, views):
+@pytest.mark.parametrize("views,m", [(17, 48), (40, 48), (128, 48), (20, 300)])
+def test_many_views_per_call(mods, monkeypatch, views, m):
     """A call of more than 16 views (device camera table, kInlineCams) renders what calls of at most
     16 views render, bit for bit (per-ray outputs), and its train step's gradient equals the sum of
-    the smaller calls' to fp32 rounding (another block order in the reduction)."""
+    the smaller calls' to fp32 rounding (another block order in the reduction). 300 spheres at
+    these sizes take the split march (its four-wave origin step included)."""
     import numpy as np
     torch, model, native, render = mods
     monkeypatch.setenv("RM_SMALL", "0")
-    sc = model.scene_tensors(model.synthetic_scene(48, 3), "cuda")
+    sc = model.scene_tensors(model.synthetic_scene(m, 3), "cuda")
     cams = model.ring_cameras(views)
     one = render.render_diff_camera(cams, 32, 32, sc, 32.0, 24)
     parts = torch.cat([render.render_diff_camera(cams[i:i + 16], 32, 32, sc, 32.0, 24) for i in range(0, views, 16)])
     assert torch.equal(one, parts)
-    tgt = render.render_diff_camera(cams, 32, 32, model.scene_tensors(model.synthetic_scene(48, 4), "cuda"), 32.0, 24)
+    tgt = render.render_diff_camera(cams, 32, 32, model.scene_tensors(model.synthetic_scene(m, 4), "cuda"), 32.0, 24)
     n = views * 32 * 32
     _, g1, _ = render.train_step_camera(cams, 32, 32, tgt, sc, 32.0, 0.3, 24, inv_count=1.0 / (3 * n))
     acc = None
