@@ -40,7 +40,7 @@ def _pack(g):
                            for k in ("centers", "colors", "radius", "light_dir", "ambient")])
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, global_views=0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import sys
@@ -56,7 +56,8 @@ def _worker(rank, world, port, out_dir):
         grads_out.copy_(torch.from_numpy(_pack(g)).to(grads_out.dtype))
         loss_out.fill_(loss_sum)
 
-    dp = ViewShardedStep(Shard(rank, world, VPG, RING), W * W, 7 * M + 4, "cpu", step_fn)
+    shard = Shard(rank, world, 0 if global_views else VPG, RING, global_views)
+    dp = ViewShardedStep(shard, W * W, 7 * M + 4, "cpu", step_fn)
     dp.buf = dp.buf.double()
     dp.grads = dp.buf[:7 * M + 4]
     dp.loss = dp.buf[7 * M + 4:]
@@ -105,3 +106,42 @@ def test_shard_rotation_covers_ring():
         for r in range(2):
             seen.update(Shard(r, 2, 1, 6).views(step))
     assert seen == set(range(6))
+
+
+@pytest.mark.timeout(300)
+def test_strong_scaling_uneven_split_equals_single_process():
+    """Strong scaling (bench.py --global-views): 3 views per step over 2 ranks (2 + 1), the
+    global-N normalisation and the one all-reduce give the single-process gradient of the step's
+    3 views; the step's views are disjoint across ranks and rotate over the ring."""
+    world, gv = 2, 3
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.spawn(_worker, args=(world, _free_port(), tmp, gv), nprocs=world, join=True)
+        orc, sc, rays, targets = _setup()
+        for step in range(3):
+            a = np.load(os.path.join(tmp, f"r0_s{step}.npy"))
+            b = np.load(os.path.join(tmp, f"r1_s{step}.npy"))
+            assert np.array_equal(a, b)
+            v0 = list(np.load(os.path.join(tmp, f"views_r0_s{step}.npy")))
+            v1 = list(np.load(os.path.join(tmp, f"views_r1_s{step}.npy")))
+            assert len(v0) == 2 and len(v1) == 1 and not set(v0) & set(v1)
+            views = v0 + v1
+            assert views == [(step * gv + j) % RING for j in range(gv)]
+            o = np.concatenate([rays[v][0] for v in views])
+            d = np.concatenate([rays[v][1] for v in views])
+            tg = np.concatenate([targets[v] for v in views])
+            _, loss_sum, g = orc.train_step(o, d, tg, sc, S, K, 0.25)
+            assert np.allclose(a[:-1], _pack(g), rtol=1e-10, atol=1e-13)
+            assert abs(a[-1] - loss_sum) <= 1e-10 * abs(loss_sum)
+
+
+def test_shard_counts_strong_and_weak():
+    from burn_raymarching_amd.parallel import Shard
+    for world, gv in ((2, 5), (3, 7), (8, 80), (8, 3)):
+        counts = [Shard(r, world, 0, 100, gv).count() for r in range(world)]
+        assert sum(counts) == gv and max(counts) - min(counts) <= 1
+        seen = []
+        for r in range(world):
+            seen += Shard(r, world, 0, 100, gv).views(4)
+        assert seen == [(4 * gv + j) % 100 for j in range(gv)]
+    weak = Shard(1, 4, 10, 80)
+    assert weak.count() == 10 and weak.views_total == 40
