@@ -25,6 +25,9 @@ torch.distributed.run the ranks come from the environment, and a WORLD_SIZE that
 
 Synthetic data (no datasets offline): scene seed 0 (BASELINE.md "Synthetic inputs"), targets
 = the seed-1 scene rendered by the forward kernel from a ring of cameras at radius 2.5, y 0.5.
+Ring position j looks from angle (49 j mod 80) / 80 of the circle (--ring-order spread), so each
+rank's contiguous slice samples the whole circle: per-slice train-call times at N = 8 differ by
+0.5 % instead of 3.5 % with angle j (tools/shard_balance.py, profiles/r04b_shard_balance.json).
 
 Extra objects on the JSON line:
   roofline      -- the dominant kernel (rm_ray_kernel<train>) timed with hipEvents from its own
@@ -84,6 +87,9 @@ def parse():
                     help="weak scaling: views per GPU per step (e.g. 10 = the 10-camera ring of BASELINE "
                          "configs[1-2] = 2,621,440 rays in one launch); exclusive with --global-views")
     ap.add_argument("--ring", type=int, default=10, help="cameras on the target ring (at least the views of a step)")
+    ap.add_argument("--ring-order", choices=["contiguous", "spread"], default="spread",
+                    help="camera angle of ring position j: angle j (contiguous) or angle (j * s) mod ring with s the "
+                         "coprime stride nearest 0.618 ring (spread: a rank's contiguous slice covers the circle)")
     ap.add_argument("--views-per-call", type=int, default=0,
                     help="views per train call (0: as many as one launch takes, up to 128 = the strong default's "
                          "80 views in one call)")
@@ -150,6 +156,18 @@ def launch_ranks(n: int) -> int:
                     q.terminate()
         time.sleep(0.05)
     return rc
+
+
+def ring_order(n: int, order: str) -> list[int]:
+    """Camera angle index of each ring position. 'spread': position j looks from angle (j * s) mod n,
+    s the stride coprime with n nearest 0.618 n (a golden-ratio sequence), so any contiguous slice
+    of positions -- a rank's views in strong scaling -- samples the whole circle."""
+    if order == "contiguous" or n <= 2:
+        return list(range(n))
+    import math
+    base = max(1, round(0.618 * n))
+    s = min((c for c in range(1, n) if math.gcd(c, n) == 1), key=lambda c: (abs(c - base), c))
+    return [(j * s) % n for j in range(n)]
 
 
 def _latest_profile(pattern: str, key: str, field: str):
@@ -234,7 +252,7 @@ def main():
     sc1 = rmm.synthetic_scene(M, seed=1, radius_range=rr)
     ring = max(args.ring, shard.views_total)
     shard.ring = ring
-    cams = rmm.ring_cameras(ring)
+    cams = [rmm.ring_cameras(ring)[a] for a in ring_order(ring, args.ring_order)]
     tgt_scene = rmm.scene_tensors(sc1)
     targets = torch.empty((ring, npix, 3), device="cuda")
     for v0 in range(0, ring, native.RM_MAX_VIEWS_PER_CALL):
@@ -487,7 +505,7 @@ def main():
                        "width": W, "height": H, "spheres": M, "march_steps": S, "smooth_k": K,
                        "views_per_gpu": vpg, "global_views": shard.views_total, "views_per_call": views_per_call,
                        "streams": nstreams,
-                       "ring": ring, "rays_per_step": rays_global, "radius_range": list(rr),
+                       "ring": ring, "ring_order": args.ring_order, "rays_per_step": rays_global, "radius_range": list(rr),
                        "color_storage": args.color_dtype, "sdf_dtype": "f32",
                        "parallelism": f"views-dp{world}" + ("" if backend == "nccl" else f" ({backend} rehearsal)")},
             "value_median": round(rays_global / (med_ms * 1e-3) / 1e6, 3),
