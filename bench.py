@@ -87,9 +87,11 @@ def parse():
                     help="weak scaling: views per GPU per step (e.g. 10 = the 10-camera ring of BASELINE "
                          "configs[1-2] = 2,621,440 rays in one launch); exclusive with --global-views")
     ap.add_argument("--ring", type=int, default=10, help="cameras on the target ring (at least the views of a step)")
-    ap.add_argument("--ring-order", choices=["contiguous", "spread"], default="spread",
+    ap.add_argument("--ring-order", choices=["contiguous", "spread"], default=None,
                     help="camera angle of ring position j: angle j (contiguous) or angle (j * s) mod ring with s the "
-                         "coprime stride nearest 0.618 ring (spread: a rank's contiguous slice covers the circle)")
+                         "coprime stride nearest 0.618 ring (spread: a rank's contiguous slice covers the circle); "
+                         "default spread for strong scaling, contiguous for weak (whose per-step view rotation, and "
+                         "so the training trajectory of the BASELINE configs, stays that of earlier rounds)")
     ap.add_argument("--views-per-call", type=int, default=0,
                     help="views per train call (0: as many as one launch takes, up to 128 = the strong default's "
                          "80 views in one call)")
@@ -121,6 +123,8 @@ def parse():
         ap.error("--global-views (strong scaling) and --views-per-gpu (weak scaling) are exclusive")
     if args.global_views is None and args.views_per_gpu is None:
         args.global_views = DEFAULT_GLOBAL_VIEWS
+    if args.ring_order is None:
+        args.ring_order = "spread" if args.global_views is not None else "contiguous"
     if args.global_views is not None and args.global_views < args.gpus:
         ap.error(f"--global-views {args.global_views} < --gpus {args.gpus}: every rank needs a view")
     return args
