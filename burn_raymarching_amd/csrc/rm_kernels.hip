@@ -2707,17 +2707,19 @@ __global__ __launch_bounds__(256) void rm_penalty_pairs(const float* __restrict_
 
 // One parameter element i of the packed layout: chain rule of the activations, the compute_loss
 // penalties (training.rs:38-82), coupled weight decay and Burn's Adam; optionally the activated
-// parameters of the updated model (scene.rs:41-45) for the next step's render. raw: the pre-step
-// parameters (a snapshot: neighbours are read); pair: the repulsion rows. Returns the element's
-// penalty-loss share.
-__device__ __forceinline__ float optimizer_elem(int i, const float* raw, float* __restrict__ raw_out,
-                                                const float* __restrict__ gact, const float* m1_in,
-                                                const float* m2_in, float* __restrict__ m1, float* __restrict__ m2,
-                                                const float* pair, int M, int step, float lr, float wd, int with_pen,
-                                                float* __restrict__ act_out, _Float16* __restrict__ col_h_out) {
-  float pen = 0.0f;
+// parameters of the updated model (scene.rs:41-45) for the next step's render. Split in two: the
+// part that depends on the pre-step parameters only (optimizer_pre: the chain-rule factor, the
+// penalties' gradient terms and loss share -- the fused iteration runs it while the gradient is
+// still being summed) and the update itself (optimizer_apply).
+struct ElemPre {
+  float fac;         // d activation / d raw (1 for centres and light)
+  float t0, t1, t2;  // penalty gradient terms, added in this order after the chain rule
+  float pen;         // the element's penalty-loss share
+};
+// raw: the pre-step parameters (a snapshot: neighbours are read); pair: the repulsion rows.
+__device__ __forceinline__ ElemPre optimizer_pre(int i, const float* raw, const float* pair, int M, int with_pen) {
+  ElemPre e{1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
   const float x = raw[i];
-  float gv = gact[i];
   const float invM = 1.0f / (float)M;
   const float rep_scale = 1e-5f / ((float)M * (float)M);
   if (i < 3 * M) {  // centers (identity activation)
@@ -2725,56 +2727,86 @@ __device__ __forceinline__ float optimizer_elem(int i, const float* raw, float* 
       const int s = i / 3, ax = i - 3 * s;
       const float cx = raw[3 * s], cy = raw[3 * s + 1], cz = raw[3 * s + 2];
       const float rs = softplusf_(raw[6 * M + s]);  // penalties use softplus without +0.01 (training.rs:41)
-      gv += 0.05f * 2.0f * x / (3.0f * M);          // [b] mean(c^2) over [M,3] * 0.05
+      e.t0 = 0.05f * 2.0f * x / (3.0f * M);         // [b] mean(c^2) over [M,3] * 0.05
       const float csq = cx * cx + cy * cy + cz * cz;
       const float dist = sqrtf(csq + 1e-6f);
       const float reach = dist + rs;                // [c] mean(mask * (|c| + r - 1.2)^2) * 5
-      if (reach > 1.2f) gv += 5.0f * invM * 2.0f * (reach - 1.2f) * (x / dist);
-      gv += rep_scale * pair[4 * s + ax];           // [d] repulsion (repulsion_row)
+      if (reach > 1.2f) e.t1 = 5.0f * invM * 2.0f * (reach - 1.2f) * (x / dist);
+      e.t2 = rep_scale * pair[4 * s + ax];          // [d] repulsion (repulsion_row)
       if (ax == 0) {
-        pen += 0.05f * csq / (3.0f * M);
-        if (reach > 1.2f) pen += 5.0f * invM * (reach - 1.2f) * (reach - 1.2f);
-        pen += rep_scale * pair[4 * s + 3];
+        e.pen += 0.05f * csq / (3.0f * M);
+        if (reach > 1.2f) e.pen += 5.0f * invM * (reach - 1.2f) * (reach - 1.2f);
+        e.pen += rep_scale * pair[4 * s + 3];
       }
     }
   } else if (i < 6 * M) {  // colors: d sigmoid = c (1 - c)
     const float c = sigmoidf_(x);
-    gv *= c * (1.0f - c);
+    e.fac = c * (1.0f - c);
   } else if (i < 7 * M) {  // radius: d (softplus + 0.01) = sigmoid
     const float sg = sigmoidf_(x);
-    gv *= sg;
+    e.fac = sg;
     if (with_pen) {
       const int s = i - 6 * M;
       const float rs = softplusf_(x);
-      gv += 0.002f * invM * (rs > 0.0f ? 1.0f : (rs < 0.0f ? -1.0f : 0.0f)) * sg;  // [a] L1
-      pen += 0.002f * invM * fabsf(rs);
+      e.t0 = 0.002f * invM * (rs > 0.0f ? 1.0f : (rs < 0.0f ? -1.0f : 0.0f)) * sg;  // [a] L1
+      e.pen += 0.002f * invM * fabsf(rs);
       if (rs > 1.0f) {  // [a] large radius
-        gv += 0.04f * invM * 2.0f * rs * sg;
-        pen += 0.04f * invM * rs * rs;
+        e.t1 = 0.04f * invM * 2.0f * rs * sg;
+        e.pen += 0.04f * invM * rs * rs;
       }
       const float cx = raw[3 * s], cy = raw[3 * s + 1], cz = raw[3 * s + 2];
       const float reach = sqrtf(cx * cx + cy * cy + cz * cz + 1e-6f) + rs;
-      if (reach > 1.2f) gv += 5.0f * invM * 2.0f * (reach - 1.2f) * sg;  // [c] w.r.t. radius
+      if (reach > 1.2f) e.t2 = 5.0f * invM * 2.0f * (reach - 1.2f) * sg;  // [c] w.r.t. radius
     }
   } else if (i >= 7 * M + 3) {  // ambient: d sigmoid (light_dir raw: identity)
     const float a = sigmoidf_(x);
-    gv *= a * (1.0f - a);
+    e.fac = a * (1.0f - a);
   }
-  // Burn Adam with coupled weight decay: g += wd * theta; moments; bias correction.
+  return e;
+}
+
+// Adam's bias corrections 1 - beta^t (Burn Adam: beta1 0.9, beta2 0.999)
+struct AdamBias {
+  float c1, c2;
+};
+__device__ __forceinline__ AdamBias adam_bias(int step) {
+  return AdamBias{1.0f - powf(0.9f, (float)step), 1.0f - powf(0.999f, (float)step)};
+}
+
+// The update of element i from its gradient g w.r.t. the activated value, its pre-step raw value
+// x and moments mo1 / mo2: gv = g fac + t0 + t1 + t2, Burn Adam with coupled weight decay
+// (g += wd theta; moments; bias correction).
+__device__ __forceinline__ void optimizer_apply(int i, const ElemPre& e, float g, float x, float mo1, float mo2,
+                                                const AdamBias& bias, float lr, float wd, int M,
+                                                float* __restrict__ raw_out, float* __restrict__ m1,
+                                                float* __restrict__ m2, float* __restrict__ act_out,
+                                                _Float16* __restrict__ col_h_out) {
+  float gv = ((g * e.fac + e.t0) + e.t1) + e.t2;
   gv = fmaf(wd, x, gv);
   const float b1 = 0.9f, b2 = 0.999f, eps = 1e-5f;
-  const float mm = fmaf(b1, m1_in[i], (1.0f - b1) * gv);
-  const float vv = fmaf(b2, m2_in[i], (1.0f - b2) * gv * gv);
+  const float mm = fmaf(b1, mo1, (1.0f - b1) * gv);
+  const float vv = fmaf(b2, mo2, (1.0f - b2) * gv * gv);
   m1[i] = mm;
   m2[i] = vv;
-  const float mh = mm / (1.0f - powf(b1, (float)step));
-  const float vh = vv / (1.0f - powf(b2, (float)step));
+  const float mh = mm / bias.c1;
+  const float vh = vv / bias.c2;
   const float xn = x - lr * (mh / (sqrtf(vh) + eps));
   raw_out[i] = xn;
   if (act_out) act_out[i] = activate_elem(xn, i, M);
   // fp16 colour models (RM_MARCH_COLOR_F16): the next render's colours, rounded to nearest
   if (col_h_out != nullptr && i >= 3 * M && i < 6 * M) col_h_out[i - 3 * M] = (_Float16)activate_elem(xn, i, M);
-  return pen;
+}
+
+// Both parts for one element; returns the element's penalty-loss share.
+__device__ __forceinline__ float optimizer_elem(int i, const float* raw, float* __restrict__ raw_out,
+                                                const float* __restrict__ gact, const float* m1_in,
+                                                const float* m2_in, float* __restrict__ m1, float* __restrict__ m2,
+                                                const float* pair, int M, int step, float lr, float wd, int with_pen,
+                                                float* __restrict__ act_out, _Float16* __restrict__ col_h_out) {
+  const ElemPre e = optimizer_pre(i, raw, pair, M, with_pen);
+  optimizer_apply(i, e, gact[i], raw[i], m1_in[i], m2_in[i], adam_bias(step), lr, wd, M, raw_out, m1, m2, act_out,
+                  col_h_out);
+  return e.pen;
 }
 
 // Pass B: one thread per parameter element (optimizer_elem); per-block penalty partials.
@@ -2800,9 +2832,10 @@ __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restri
 }
 
 // The optimizer step of a small model (M <= kOptSmallMaxM) in one block: the pre-step parameters
-// and moments into LDS (the snapshot rm_penalty_pairs writes), the repulsion rows of
-// training.rs:73-82 (four threads per sphere, their partials added in order), then optimizer_elem
-// per element and the penalty sum (block tree reduction). One launch instead of three.
+// into LDS (the snapshot rm_penalty_pairs writes), the repulsion rows of training.rs:73-82 (four
+// threads per sphere, their partials added in order), optimizer_pre per element and the penalty
+// sum (block tree reduction) -- everything that does not need the gradient (opt_small_pre) --
+// then optimizer_apply per element (opt_small_post). One launch instead of three.
 // OptPrefetch: the block's loads of the parameters and moments (elements tid and tid + 256),
 // issued before whatever the block does next (the fused iteration's final reduction) so that
 // their latency overlaps it.
@@ -2822,30 +2855,27 @@ __device__ __forceinline__ OptPrefetch opt_prefetch(const float* raw, const floa
   }
   return f;
 }
+struct OptPre {
+  ElemPre e[2];  // elements tid and tid + 256
+  AdamBias bias;
+};
 
-// The body, for a 256-thread block (also the tail of the fused training iteration, rm_small.h).
-__device__ __forceinline__ void optimizer_small_block(const OptPrefetch& pf, float* __restrict__ raw,
-                                                      const float* gact, float* __restrict__ m1,
-                                                      float* __restrict__ m2, int M, int step, float lr, float wd,
-                                                      int with_pen, float* __restrict__ loss_penalty,
-                                                      float* __restrict__ act_out, _Float16* __restrict__ col_h_out) {
+// The gradient-independent part, for a 256-thread block (every thread calls it: block barriers).
+__device__ __forceinline__ OptPre opt_small_pre(const OptPrefetch& pf, int M, int step, int with_pen,
+                                                float* __restrict__ loss_penalty) {
   static_assert(7 * kOptSmallMaxM + 4 <= 512, "two elements per thread");
   __shared__ float snap[7 * kOptSmallMaxM + 4];
-  __shared__ float sm1[7 * kOptSmallMaxM + 4];
-  __shared__ float sm2[7 * kOptSmallMaxM + 4];
   __shared__ float part[4][kOptSmallMaxM][4];
   __shared__ float pair[kOptSmallMaxM * 4];
   __shared__ float red[4 * 256];
   const int tid = threadIdx.x;
   const int n = 7 * M + 4;
+  OptPre o;
+  o.bias = adam_bias(step);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
     const int i = tid + 256 * h;
-    if (i < n) {
-      snap[i] = pf.x[h];
-      sm1[i] = pf.a[h];
-      sm2[i] = pf.b[h];
-    }
+    if (i < n) snap[i] = pf.x[h];
   }
   __syncthreads();
   if (with_pen) {
@@ -2864,12 +2894,32 @@ __device__ __forceinline__ void optimizer_small_block(const OptPrefetch& pf, flo
     __syncthreads();
   }
   float pen = 0.0f;
-  for (int i = tid; i < n; i += 256)
-    pen += optimizer_elem(i, snap, raw, gact, sm1, sm2, m1, m2, pair, M, step, lr, wd, with_pen, act_out, col_h_out);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = tid + 256 * h;
+    o.e[h] = i < n ? optimizer_pre(i, snap, pair, M, with_pen) : ElemPre{1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    pen += o.e[h].pen;
+  }
   if (loss_penalty != nullptr) {
     float v[4] = {pen, 0.0f, 0.0f, 0.0f};
     block_sum4(v, red);
     if (tid == 0) loss_penalty[0] = v[0];
+  }
+  return o;
+}
+
+// The update on the gradient g (w.r.t. the activated values) of elements tid and tid + 256.
+__device__ __forceinline__ void opt_small_post(const OptPre& o, const OptPrefetch& pf, const float (&g)[2],
+                                               float* __restrict__ raw, float* __restrict__ m1,
+                                               float* __restrict__ m2, int M, float lr, float wd,
+                                               float* __restrict__ act_out, _Float16* __restrict__ col_h_out) {
+  const int n = 7 * M + 4;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = (int)threadIdx.x + 256 * h;
+    if (i < n)
+      optimizer_apply(i, o.e[h], g[h], pf.x[h], pf.a[h], pf.b[h], o.bias, lr, wd, M, raw, m1, m2, act_out,
+                      col_h_out);
   }
 }
 
@@ -2878,8 +2928,11 @@ __global__ __launch_bounds__(256) void rm_optimizer_small(float* __restrict__ ra
                                                           int step, float lr, float wd, int with_pen,
                                                           float* __restrict__ loss_penalty, float* __restrict__ act_out,
                                                           _Float16* __restrict__ col_h_out) {
-  optimizer_small_block(opt_prefetch(raw, m1, m2, M), raw, gact, m1, m2, M, step, lr, wd, with_pen, loss_penalty,
-                        act_out, col_h_out);
+  const OptPrefetch pf = opt_prefetch(raw, m1, m2, M);
+  const int n = 7 * M + 4, i0 = (int)threadIdx.x;
+  const float g[2] = {i0 < n ? gact[i0] : 0.0f, i0 + 256 < n ? gact[i0 + 256] : 0.0f};
+  const OptPre o = opt_small_pre(pf, M, step, with_pen, loss_penalty);
+  opt_small_post(o, pf, g, raw, m1, m2, M, lr, wd, act_out, col_h_out);
 }
 
 __global__ void rm_sum_small(const float* __restrict__ parts, int n, float* __restrict__ out) {
@@ -2916,6 +2969,7 @@ struct rm_context {
   hipEvent_t cam_ev[32] = {};               // slot k's copy has run (kCamRing slots)
   int cam_slot = 0;
   float* batch = nullptr;                   // rm_train_iteration's unfused path: the drawn batch (9 floats/ray)
+  float* opt_pre = nullptr;                 // rm_train_iteration: the optimizer part of the launch's extra block
   size_t batch_bytes = 0;
   size_t rec_bytes = 0;
   long long stats_blocks = 0;               // ray blocks launched while stats are on
@@ -3255,9 +3309,9 @@ int run_small(rm_context* ctx, const Call& c, KArgs& a, long long n) {
 #ifdef RM_BLOCK_TRACE
     if (!ctx->btrace)
       RM_HIP(ctx, hipMalloc(&ctx->btrace, sizeof(unsigned long long) * kTraceWords * kWaves * (size_t)kMaxBlocksPerLaunch));
-    RM_HIP(ctx, hipMemsetAsync(ctx->btrace, 0, sizeof(unsigned long long) * kTraceWords * kWaves * (size_t)nb, ctx->stream));
+    RM_HIP(ctx, hipMemsetAsync(ctx->btrace, 0, sizeof(unsigned long long) * kTraceWords * kWaves * (size_t)(nb + 1), ctx->stream));
     a.btrace = ctx->btrace;
-    ctx->btrace_waves = nb * kWaves;
+    ctx->btrace_waves = (nb + (c.fused ? 1 : 0)) * kWaves;
 #endif
     SmallArgs sa;
     std::memset(&sa, 0, sizeof sa);
@@ -3272,9 +3326,13 @@ int run_small(rm_context* ctx, const Call& c, KArgs& a, long long n) {
       ctx->stats_blocks += nb;
       ctx->stats_waves += nb * kWaves;
     }
+    if (c.fused) {  // the extra block's optimizer part (rm_small.h)
+      if (!ctx->opt_pre) RM_HIP(ctx, hipMalloc(&ctx->opt_pre, sizeof(float) * (4 * kOptPreStride + 2)));
+      sa.opt_pre = ctx->opt_pre;
+    }
     hipEvent_t ev0, ev1;
     if ((rc = next_events(ctx, ev0, ev1)) != RM_OK) return rc;
-    const dim3 grid((unsigned)nb);
+    const dim3 grid((unsigned)(nb + (c.fused ? 1 : 0)));
     if (c.fused && lpr == 2) launch_small_m<kTrain, true, 2>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
     else if (c.fused) launch_small_m<kTrain, true>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
     else if (c.mode == kFwd) launch_small_m<kFwd>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
@@ -3771,11 +3829,12 @@ void rm_destroy(rm_context* ctx) {
     if (ctx->ocnt) (void)hipFree(ctx->ocnt);
     if (ctx->rec) (void)hipFree(ctx->rec);
   }
-  if (ctx->arrivals || ctx->red_arrivals || ctx->batch || ctx->cams_dev) {
+  if (ctx->arrivals || ctx->red_arrivals || ctx->batch || ctx->cams_dev || ctx->opt_pre) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->arrivals) (void)hipFree(ctx->arrivals);
     if (ctx->red_arrivals) (void)hipFree(ctx->red_arrivals);
     if (ctx->batch) (void)hipFree(ctx->batch);
+    if (ctx->opt_pre) (void)hipFree(ctx->opt_pre);
     if (ctx->cams_dev) (void)hipFree(ctx->cams_dev);
     if (ctx->cams_pin) (void)hipHostFree(ctx->cams_pin);
     for (hipEvent_t& e : ctx->cam_ev)

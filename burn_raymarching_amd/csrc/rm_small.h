@@ -43,14 +43,17 @@ struct SmallArgs {
   const int32_t* fg;
   long long num_src, num_fg, n_uniform;
   unsigned long long key;
-  float* raw;             // optimizer (optimizer_small_block): raw parameters, moments
+  float* raw;             // optimizer (opt_small_pre / opt_small_post): raw parameters, moments
   float* m1;
   float* m2;
   int step, with_pen;
   float lr, wd;
   float* loss_penalty;    // nullable
   float* act_out;         // the next render's activated parameters (the scene this launch read)
+  float* opt_pre;         // FUSED: [4][kOptPreStride] chain-rule factor and penalty terms per element,
+                          // then Adam's two bias corrections (the extra block -> the final block)
 };
+constexpr int kOptPreStride = 256;  // >= 7 kSmallMaxM + 4 elements
 
 // Per-sphere march data in registers, pair p = spheres (2p, 2p + 1): gx = -2c, cc = |c|^2
 // (expansion form, scene.rs:66-71), kr = kappa r (kappa = smooth_k log2 e).
@@ -125,6 +128,144 @@ __device__ __forceinline__ float small_softmin_half(const float p[3], const Smal
   return -(flog2(fmaxf(s, 1e-8f)) + m) * inv_kappa;
 }
 
+// The arrival of a block (after its write-through record stores): every storing wave drained
+// before the block barrier, one lane's agent-scope add to the launch's counter. True in the block
+// that arrives last (MI355X_MICROARCH.md, inter-workgroup visibility).
+__device__ __forceinline__ bool small_arrive(const SmallArgs& sa, int* s_last) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(sa.arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_last = prev == gridDim.x - 1 ? 1 : 0;
+  }
+  __syncthreads();
+  return *s_last != 0;
+}
+
+// The last block: sum the nrows blocks' records and write the gradients (rm_finalize_grads'
+// layout and light-direction Jacobian; ldn / ldlen: ld / |ld| and |ld| of the scene's light_dir,
+// as the shade stage forms them); FUSED: then the optimizer update on that gradient, with the
+// gradient-independent part the launch's extra block left in sa.opt_pre. s_red: the kernel's
+// cross-wave LDS buffer (free by now).
+template <bool FUSED>
+__device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa, int nrows, float* s_red,
+                                            const float (&ldn)[3], float ldlen) {
+  const int tid = threadIdx.x;
+  const int M = a.M, Mpad = a.Mpad;
+  const int nneed = M * 8 + 8;  // columns of the real spheres, then the scalars
+  auto col_of = [&](int idx) { return idx < M * 8 ? idx : Mpad * 8 + (idx - M * 8); };
+  // FUSED: the optimizer's parameters and moments load while the block sums the records
+  OptPrefetch pf;
+  if constexpr (FUSED) pf = opt_prefetch(sa.raw, sa.m1, sa.m2, M);
+  // The records are read with write-through-cache (sc1) loads only, stored sc1 by every block,
+  // each storing wave drained (vmcnt(0)) before the barrier behind which one lane adds to the one
+  // counter whose last add tells this block: the hand-off row of MI355X_MICROARCH.md
+  // (inter-workgroup visibility) under which sc1 loads may replace the agent-scope acquire. The
+  // acquire is kept (sa.acquire, env RM_SMALL_ACQUIRE=0 drops it): without it the tail measured
+  // the same (tools/small_trace.py: 4.96 vs 5.12 us at 128 blocks).
+  if (sa.acquire && tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  RM_TRACE(11, __builtin_amdgcn_s_memrealtime());
+  // FUSED: the extra block's optimizer part, loaded with the records (the same hand-off)
+  [[maybe_unused]] OptPre opre;
+  if constexpr (FUSED) {
+    const int n = 7 * M + 4;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int i = tid + 256 * h;
+      float v[4] = {1.0f, 0.0f, 0.0f, 0.0f};
+      if (i < n)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          v[k] = __hip_atomic_load(sa.opt_pre + k * kOptPreStride + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      opre.e[h] = ElemPre{v[0], v[1], v[2], v[3], 0.0f};
+    }
+    opre.bias.c1 = __hip_atomic_load(sa.opt_pre + 4 * kOptPreStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    opre.bias.c2 = __hip_atomic_load(sa.opt_pre + 4 * kOptPreStride + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  // each needed column is summed by `chains` threads (rows b = k mod chains, in order), the chains
+  // then added in order: a fixed order for every launch of this size. The write-through loads
+  // miss the local L2 (~1 us each round trip): kFinBatch rows in flight per thread, so that a
+  // launch of up to kSmallFinalMaxBlocks blocks takes one or two rounds.
+  constexpr int kFinBatch = 32;
+  const int nb = nrows;
+  const int chains = max(1, min(8, kBlock / nneed));
+  for (int w = tid; w < nneed * chains; w += kBlock) {
+    const int idx = w % nneed, ch = w / nneed;
+    const long long e = col_of(idx);
+    float acc = 0.0f;
+    for (int b0 = ch; b0 < nb; b0 += kFinBatch * chains) {
+      float v[kFinBatch];
+#pragma unroll
+      for (int u = 0; u < kFinBatch; ++u) {
+        const int b = b0 + u * chains;
+        v[u] = b < nb ? __hip_atomic_load(a.partials + (long long)b * a.rec + e, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT)
+                      : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < kFinBatch; ++u)
+        if (b0 + u * chains < nb) acc += v[u];
+    }
+    s_red[ch * nneed + idx] = acc;
+  }
+  __syncthreads();
+  RM_TRACE(2, __builtin_amdgcn_s_memrealtime());
+  const FinalArgs& f = sa.fin;
+  auto total = [&](int idx) {
+    float v = s_red[idx];
+    for (int ch = 1; ch < chains; ++ch) v += s_red[ch * nneed + idx];
+    return v;
+  };
+  // FUSED: the gradient also goes to LDS in the packed layout the optimizer reads
+  [[maybe_unused]] float* s_gact = nullptr;
+  if constexpr (FUSED) {
+    __shared__ float s_gact_buf[7 * kSmallMaxM + 4];
+    s_gact = s_gact_buf;
+  }
+  for (int idx = tid; idx < M * 8; idx += kBlock) {
+    const int j = idx >> 3, comp = idx & 7;
+    if (comp == 7) continue;
+    float* dst = comp < 3 ? (f.gc ? f.gc + 3 * j + comp : nullptr)
+                          : (comp == 3 ? (f.gr ? f.gr + j : nullptr) : (f.gcol ? f.gcol + 3 * j + (comp - 4) : nullptr));
+    const float v = total(idx);
+    if (dst) store_or_add(dst, v, f.accumulate);
+    if constexpr (FUSED) s_gact[comp < 3 ? 3 * j + comp : (comp == 3 ? 6 * M + j : 3 * M + 3 * j + (comp - 4))] = v;
+  }
+  if (tid == 0) {
+    const float sc[5] = {total(M * 8), total(M * 8 + 1), total(M * 8 + 2), total(M * 8 + 3), total(M * 8 + 4)};
+    if (f.gld) {
+      const float proj = ldn[0] * sc[0] + ldn[1] * sc[1] + ldn[2] * sc[2];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float gv = (sc[c] - ldn[c] * proj) / ldlen;
+        store_or_add(f.gld + c, gv, f.accumulate);
+        if constexpr (FUSED) s_gact[7 * M + c] = gv;
+      }
+    }
+    if constexpr (FUSED) s_gact[7 * M + 3] = sc[3];
+    if (f.gamb) store_or_add(f.gamb, sc[3], f.accumulate);
+    if (f.loss_sum) store_or_add(f.loss_sum, sc[4], f.accumulate);
+    __hip_atomic_store(sa.arrivals, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+  }
+  RM_TRACE(9, __builtin_amdgcn_s_memrealtime());
+  RM_TRACE(1, __builtin_amdgcn_s_memrealtime());
+  if constexpr (FUSED) {
+    // the optimizer step (rm_optimizer_step: penalties + Adam, train.rs:198) on the gradient just
+    // summed (its LDS copy in the packed layout). Every other block has arrived, so nothing reads
+    // the activated or raw parameters any more when act_out and raw are overwritten.
+    __syncthreads();
+    const int n = 7 * M + 4;
+    const float g[2] = {tid < n ? s_gact[tid] : 0.0f, tid + 256 < n ? s_gact[tid + 256] : 0.0f};
+    opt_small_post(opre, pf, g, sa.raw, sa.m1, sa.m2, M, sa.lr, sa.wd, sa.act_out, nullptr);
+    RM_TRACE(10, __builtin_amdgcn_s_memrealtime());
+    RM_TRACE(1, __builtin_amdgcn_s_memrealtime());
+  }
+}
+
 // LPR (lanes per ray, train steps): 2 -- the S march steps run with each ray's spheres split over
 // two lanes (128 rays per block, twice the waves: the reference loop's 16,384-ray batch fills
 // half of the SIMDs instead of a quarter), then the rays go through LDS to waves 0-1, which run
@@ -152,6 +293,40 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
   // tools/small_trace.py)
   RM_TRACE(0, __builtin_amdgcn_s_memrealtime());
   RM_TRACE(3, (unsigned long long)blockIdx.x);
+  if constexpr (FUSED) {
+    // the launch's extra last block: the optimizer's gradient-independent part (snapshot,
+    // repulsion rows, chain-rule factors, penalty terms and loss, Adam's bias corrections) on a CU
+    // of its own while the ray blocks run, handed to the final block through sa.opt_pre
+    // (write-through stores before the arrival, as the records)
+    if (blockIdx.x == gridDim.x - 1) {
+      const OptPrefetch pf = opt_prefetch(sa.raw, sa.m1, sa.m2, M);
+      const OptPre o = opt_small_pre(pf, M, sa.step, sa.with_pen, sa.loss_penalty);
+      const int n = 7 * M + 4;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int i = tid + 256 * h;
+        if (i < n) {
+          const float v[4] = {o.e[h].fac, o.e[h].t0, o.e[h].t1, o.e[h].t2};
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            __hip_atomic_store(sa.opt_pre + k * kOptPreStride + i, v[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      if (tid == 0) {
+        __hip_atomic_store(sa.opt_pre + 4 * kOptPreStride, o.bias.c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(sa.opt_pre + 4 * kOptPreStride + 1, o.bias.c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // the final block's light Jacobian, if this block arrives last (the shade stage's expressions)
+      const float ld0 = a.light_dir[0], ld1 = a.light_dir[1], ld2 = a.light_dir[2];
+      const float ldlen = sqrtf(ld0 * ld0 + ld1 * ld1 + ld2 * ld2);
+      const float ldn[3] = {ld0 / ldlen, ld1 / ldlen, ld2 / ldlen};
+      const bool last = small_arrive(sa, &s_last);
+      RM_TRACE(8, __builtin_amdgcn_s_memrealtime());
+      RM_TRACE(1, __builtin_amdgcn_s_memrealtime());
+      if (last) small_final<FUSED>(a, sa, (int)gridDim.x - 1, s_red, ldn, ldlen);
+      return;
+    }
+  }
 
   // ---- sphere data of the activated scene (scene.rs:41-45 values), padding spheres far away
   if (tid < MB) {
@@ -450,114 +625,9 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
     __hip_atomic_store(rec + e, block_sum(e), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 
-  // ---- last block: sum the blocks' records and write the gradients (rm_finalize_grads' layout
-  // and light-direction Jacobian). Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility):
-  // write-through record stores, drained by every storing wave before the block barrier; one
-  // lane's agent-scope arrival; the block whose arrival is the last runs an agent-scope acquire
-  // before its loads.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(sa.arrivals, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = prev == gridDim.x - 1 ? 1 : 0;
-  }
-  __syncthreads();
+  const bool last = small_arrive(sa, &s_last);
   RM_TRACE(8, __builtin_amdgcn_s_memrealtime());
   RM_TRACE(1, __builtin_amdgcn_s_memrealtime());
-  if (!s_last) return;
-  // FUSED: the optimizer's parameters and moments load while the block sums the records
-  OptPrefetch pf;
-  if constexpr (FUSED) pf = opt_prefetch(sa.raw, sa.m1, sa.m2, M);
-  // The records are read with write-through-cache (sc1) loads only, stored sc1 by every block,
-  // each storing wave drained (vmcnt(0)) before the barrier behind which one lane adds to the one
-  // counter whose last add tells this block: the hand-off row of MI355X_MICROARCH.md
-  // (inter-workgroup visibility) under which sc1 loads may replace the agent-scope acquire. The
-  // acquire is kept (sa.acquire, env RM_SMALL_ACQUIRE=0 drops it): without it the tail measured
-  // the same (tools/small_trace.py: 4.96 vs 5.12 us at 128 blocks).
-  if (sa.acquire && tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  RM_TRACE(11, __builtin_amdgcn_s_memrealtime());
-  // each needed column is summed by `chains` threads (rows b = k mod chains, in order), the chains
-  // then added in order: a fixed order for every launch of this size. The write-through loads
-  // miss the local L2 (~1 us each round trip): kFinBatch rows in flight per thread, so that a
-  // launch of up to kSmallFinalMaxBlocks blocks takes one or two rounds.
-  constexpr int kFinBatch = 32;
-  const int nb = gridDim.x;
-  const int chains = max(1, min(8, kBlock / nneed));
-  for (int w = tid; w < nneed * chains; w += kBlock) {
-    const int idx = w % nneed, ch = w / nneed;
-    const long long e = col_of(idx);
-    float acc = 0.0f;
-    for (int b0 = ch; b0 < nb; b0 += kFinBatch * chains) {
-      float v[kFinBatch];
-#pragma unroll
-      for (int u = 0; u < kFinBatch; ++u) {
-        const int b = b0 + u * chains;
-        v[u] = b < nb ? __hip_atomic_load(a.partials + (long long)b * a.rec + e, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT)
-                      : 0.0f;
-      }
-#pragma unroll
-      for (int u = 0; u < kFinBatch; ++u)
-        if (b0 + u * chains < nb) acc += v[u];
-    }
-    s_red[ch * nneed + idx] = acc;
-  }
-  __syncthreads();
-  RM_TRACE(2, __builtin_amdgcn_s_memrealtime());
-  const FinalArgs& f = sa.fin;
-  auto total = [&](int idx) {
-    float v = s_red[idx];
-    for (int ch = 1; ch < chains; ++ch) v += s_red[ch * nneed + idx];
-    return v;
-  };
-  // FUSED: the gradient also goes to LDS in the packed layout the optimizer reads
-  [[maybe_unused]] float* s_gact = nullptr;
-  if constexpr (FUSED) {
-    __shared__ float s_gact_buf[7 * kSmallMaxM + 4];
-    s_gact = s_gact_buf;
-  }
-  for (int idx = tid; idx < M * 8; idx += kBlock) {
-    const int j = idx >> 3, comp = idx & 7;
-    if (comp == 7) continue;
-    float* dst = comp < 3 ? (f.gc ? f.gc + 3 * j + comp : nullptr)
-                          : (comp == 3 ? (f.gr ? f.gr + j : nullptr) : (f.gcol ? f.gcol + 3 * j + (comp - 4) : nullptr));
-    const float v = total(idx);
-    if (dst) store_or_add(dst, v, f.accumulate);
-    if constexpr (FUSED) s_gact[comp < 3 ? 3 * j + comp : (comp == 3 ? 6 * M + j : 3 * M + 3 * j + (comp - 4))] = v;
-  }
-  if (tid == 0) {
-    const float sc[5] = {total(M * 8), total(M * 8 + 1), total(M * 8 + 2), total(M * 8 + 3), total(M * 8 + 4)};
-    if (f.gld) {
-      const float l0 = f.light_dir[0], l1 = f.light_dir[1], l2 = f.light_dir[2];
-      const float len = sqrtf(l0 * l0 + l1 * l1 + l2 * l2);
-      const float ln[3] = {l0 / len, l1 / len, l2 / len};
-      const float proj = ln[0] * sc[0] + ln[1] * sc[1] + ln[2] * sc[2];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const float gv = (sc[c] - ln[c] * proj) / len;
-        store_or_add(f.gld + c, gv, f.accumulate);
-        if constexpr (FUSED) s_gact[7 * M + c] = gv;
-      }
-    }
-    if constexpr (FUSED) s_gact[7 * M + 3] = sc[3];
-    if (f.gamb) store_or_add(f.gamb, sc[3], f.accumulate);
-    if (f.loss_sum) store_or_add(f.loss_sum, sc[4], f.accumulate);
-    __hip_atomic_store(sa.arrivals, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
-  }
-  RM_TRACE(9, __builtin_amdgcn_s_memrealtime());
-  RM_TRACE(1, __builtin_amdgcn_s_memrealtime());
-  if constexpr (FUSED) {
-    // the optimizer step (rm_optimizer_step: penalties + Adam, train.rs:198) on the gradient just
-    // summed (its LDS copy in the packed layout). Every other block has arrived, so nothing reads
-    // the activated parameters any more when act_out overwrites them.
-    __syncthreads();
-    optimizer_small_block(pf, sa.raw, s_gact, sa.m1, sa.m2, M, sa.step, sa.lr, sa.wd, sa.with_pen, sa.loss_penalty,
-                          sa.act_out, nullptr);
-    RM_TRACE(10, __builtin_amdgcn_s_memrealtime());
-    RM_TRACE(1, __builtin_amdgcn_s_memrealtime());
-  }
+  if (!last) return;
+  small_final<FUSED>(a, sa, FUSED ? (int)gridDim.x - 1 : (int)gridDim.x, s_red, ldn, ldlen);
 }

@@ -73,8 +73,15 @@ def main():
     tr = tr[tr[:, 0] != 0]
     base = tr[:, 0].min()
     us = lambda c: (tr[:, c] - base) / 100.0  # noqa: E731
+    # the fused launch's extra block (the optimizer's gradient-independent part) has no ray phases
+    extra = tr[:, 4] == 0
+    last_arrival = float(us(8).max())
+    span = float(us(1).max())
+    pre = {"optimizer_part_us": float((us(8)[extra] - us(0)[extra]).max()),
+           "optimizer_part_arrival_us": float(us(8)[extra].max())} if extra.any() else {}
+    tr_all, tr = tr, tr[~extra]
     t0, t4, t5, t6, t7, t8 = us(0), us(4), us(5), us(6), us(7), us(8)
-    res = {"waves": int(len(tr)), "span_us": float(us(1).max()),
+    res = {"waves": int(len(tr)), "span_us": span, **pre,
            "start_spread_us": float(t0.max()),
            "phase_us_mean": {"setup": float((t4 - t0).mean()), "march": float((t5 - t4).mean()),
                              "post_march": float((t6 - t5).mean()), "backward": float((t7 - t6).mean()),
@@ -82,7 +89,8 @@ def main():
            "phase_us_max": {"setup": float((t4 - t0).max()), "march": float((t5 - t4).max()),
                             "post_march": float((t6 - t5).max()), "backward": float((t7 - t6).max()),
                             "record_arrival": float((t8 - t7).max())},
-           "last_arrival_us": float(t8.max())}
+           "last_arrival_us": last_arrival}
+    tr = tr_all
     last = tr[:, 9] != 0
     if last.any():
         t9, t10 = us(9)[last], us(10)[last]
