@@ -27,6 +27,9 @@
 #pragma once
 
 constexpr int kSmallMaxM = 32;             // spheres handled by the small kernel
+#ifndef RM_SMALL_FIN_BATCH
+#define RM_SMALL_FIN_BATCH 32  // record rows in flight per thread in the final block's sums
+#endif
 constexpr int kSmallFinalMaxBlocks = 128;  // in-kernel final reduction up to this many blocks
 
 struct SmallArgs {
@@ -190,7 +193,7 @@ __device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa,
   // then added in order: a fixed order for every launch of this size. The write-through loads
   // miss the local L2 (~1 us each round trip): kFinBatch rows in flight per thread, so that a
   // launch of up to kSmallFinalMaxBlocks blocks takes one or two rounds.
-  constexpr int kFinBatch = 32;
+  constexpr int kFinBatch = RM_SMALL_FIN_BATCH;
   const int nb = nrows;
   const int chains = max(1, min(8, kBlock / nneed));
   for (int w = tid; w < nneed * chains; w += kBlock) {
@@ -235,20 +238,23 @@ __device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa,
     if (dst) store_or_add(dst, v, f.accumulate);
     if constexpr (FUSED) s_gact[comp < 3 ? 3 * j + comp : (comp == 3 ? 6 * M + j : 3 * M + 3 * j + (comp - 4))] = v;
   }
-  if (tid == 0) {
-    const float sc[5] = {total(M * 8), total(M * 8 + 1), total(M * 8 + 2), total(M * 8 + 3), total(M * 8 + 4)};
+  // the scalars: lanes 0-2 the light direction's three components (each forms the same
+  // projection), lane 3 ambient, loss and the counter reset
+  if (tid < 3) {
     if (f.gld) {
+      const float sc[3] = {total(M * 8), total(M * 8 + 1), total(M * 8 + 2)};
       const float proj = ldn[0] * sc[0] + ldn[1] * sc[1] + ldn[2] * sc[2];
-#pragma unroll
-      for (int c = 0; c < 3; ++c) {
-        const float gv = (sc[c] - ldn[c] * proj) / ldlen;
-        store_or_add(f.gld + c, gv, f.accumulate);
-        if constexpr (FUSED) s_gact[7 * M + c] = gv;
-      }
+      const float mine = tid == 0 ? sc[0] : (tid == 1 ? sc[1] : sc[2]);
+      const float ln = tid == 0 ? ldn[0] : (tid == 1 ? ldn[1] : ldn[2]);
+      const float gv = (mine - ln * proj) / ldlen;
+      store_or_add(f.gld + tid, gv, f.accumulate);
+      if constexpr (FUSED) s_gact[7 * M + tid] = gv;
     }
-    if constexpr (FUSED) s_gact[7 * M + 3] = sc[3];
-    if (f.gamb) store_or_add(f.gamb, sc[3], f.accumulate);
-    if (f.loss_sum) store_or_add(f.loss_sum, sc[4], f.accumulate);
+  } else if (tid == 3) {
+    const float s3 = total(M * 8 + 3), s4 = total(M * 8 + 4);
+    if constexpr (FUSED) s_gact[7 * M + 3] = s3;
+    if (f.gamb) store_or_add(f.gamb, s3, f.accumulate);
+    if (f.loss_sum) store_or_add(f.loss_sum, s4, f.accumulate);
     __hip_atomic_store(sa.arrivals, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
   }
   RM_TRACE(9, __builtin_amdgcn_s_memrealtime());
