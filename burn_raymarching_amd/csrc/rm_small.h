@@ -57,6 +57,7 @@ struct SmallArgs {
                           // then Adam's two bias corrections (the extra block -> the final block)
 };
 constexpr int kOptPreStride = 256;  // >= 7 kSmallMaxM + 4 elements
+static_assert(7 * kSmallMaxM + 4 <= kOptPreStride, "one opt_pre column per element");
 
 // Per-sphere march data in registers, pair p = spheres (2p, 2p + 1): gx = -2c, cc = |c|^2
 // (expansion form, scene.rs:66-71), kr = kappa r (kappa = smooth_k log2 e).
@@ -375,6 +376,16 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
     else setup_ray<false>(a, ri, o, d, view);
     ti = ri;
   }
+  // train steps: the loss target, loaded here so that its latency (a random row in the fused
+  // iteration) hides behind the march instead of opening the backward
+  float tgv[3] = {0.0f, 0.0f, 0.0f};
+  if constexpr (MODE == kTrain) {
+    const float* tgt = FUSED ? sa.src_tgt : a.targets;
+    if (valid) {
+#pragma unroll
+      for (int c = 0; c < 3; ++c) tgv[c] = tgt[3 * ti + c];
+    }
+  }
   __syncthreads();
   auto load_spheres = [&](auto& S, int first) {  // pairs of spheres first, first + 1, ... from LDS
     constexpr int n = sizeof(S.gx) / sizeof(S.gx[0]);
@@ -400,7 +411,7 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
       t = fminf(t + small_softmin_half<MB / 2>(p, SH, kappa, inv_kappa), kTMax);
     }
     // the rays to waves 0-1, one per lane: origin, direction, t, rows
-    __shared__ float s_rf[8][RPB];
+    __shared__ float s_rf[10][RPB];
     __shared__ long long s_rr[2][RPB];
     const int rl = tid >> 1;
     if ((tid & 1) == 0) {
@@ -411,6 +422,9 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
       s_rf[4][rl] = d[1];
       s_rf[5][rl] = d[2];
       s_rf[6][rl] = t;
+      s_rf[7][rl] = tgv[0];
+      s_rf[8][rl] = tgv[1];
+      s_rf[9][rl] = tgv[2];
       s_rr[0][rl] = ri;
       s_rr[1][rl] = ti;
     }
@@ -425,6 +439,8 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
       d[c] = s_rf[3 + c][r2];
     }
     t = s_rf[6][r2];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) tgv[c] = s_rf[7 + c][r2];
     ri = s_rr[0][r2];
     ti = s_rr[1][r2];
     li = blk * RPB + r2;
@@ -524,8 +540,7 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
       g[1] = a.gout[3 * ri + 1];
       g[2] = a.gout[3 * ri + 2];
     } else {
-      const float* tgt = FUSED ? sa.src_tgt : a.targets;
-      const float t0 = tgt[3 * ti], t1 = tgt[3 * ti + 1], t2 = tgt[3 * ti + 2];
+      const float t0 = tgv[0], t1 = tgv[1], t2 = tgv[2];
       const float W = (t0 + t1 + t2) > 0.01f ? 10.0f : fmaf(a.progress, 4.0f, 1.0f);
       const float tg[3] = {t0, t1, t2};
 #pragma unroll
