@@ -320,7 +320,8 @@ int rm_optimizer_step_f16(rm_context* ctx, float* raw_packed, const float* grad_
  *      with_penalties, loss_penalty nullable) writing the updated activated parameters back into
  *      act_packed, as rm_optimizer_step with act_out = act_packed.
  * Models of up to 32 spheres and batches of up to 16,384 rays run as ONE launch (the small-scene
- * kernel draws and gathers its rays and its last block runs the optimizer; env
+ * kernel draws and gathers its rays, an extra block of the launch runs the optimizer's
+ * gradient-independent part beside the ray blocks and the last block applies the update; env
  * RM_FUSED_ITER=0 turns this off); other sizes run the three calls. fp32 colour models only.
  * Not for data-parallel training: the gradient is consumed before it could be all-reduced. */
 int rm_train_iteration(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
