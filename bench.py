@@ -105,6 +105,17 @@ def parse():
                          "0.03-0.12 up to 256 spheres, 0.02-0.06 up to 1024, 0.01-0.04 beyond)")
     ap.add_argument("--color-dtype", choices=["f32", "f16"], default="f32",
                     help="f16: fp16 colour / fp32 SDF (BASELINE configs[4], RM_MARCH_COLOR_F16)")
+    ap.add_argument("--cameras", default=None,
+                    help="cameras.json (the reference's data/cameras.json schema): its poses replace the synthetic "
+                         "ring (BASELINE configs[1]: '10 views (data/cameras.json)')")
+    ap.add_argument("--targets", choices=["synthetic", "dango", "files"], default="synthetic",
+                    help="synthetic: the seed-1 scene rendered by the forward kernel; dango: the generate.rs scene "
+                         "rendered by the renderer.rs kernel at WxH (what generate.rs writes at that size); files: "
+                         "the PNGs cameras.json names (their size must be WxH)")
+    ap.add_argument("--scene-json", default=None,
+                    help="start from this scene.json (train.rs:238-262 layout, radius + 0.01 re-added as scene.rs:43) "
+                         "instead of the synthetic seed-0 scene; --spheres is taken from the file (e.g. a model grown "
+                         "by `rm_train train --split-scale 0 --split-move 0`, BASELINE configs[4])")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--kernel-timing", choices=["on", "off"], default="on",
@@ -186,6 +197,40 @@ def _latest_profile(pattern: str, key: str, field: str):
     return None, None
 
 
+# generate.rs:29-40: the target scene of the reference's data/ ("dango")
+DANGO = {"centers": [[-0.3, 0.0, 0.0], [0.0, 0.0, 0.0], [0.3, 0.0, 0.0]],
+         "colors": [[1.0, 0.0, 0.0], [0.0, 1.0, 0.0], [0.0, 0.0, 1.0]], "radius": [0.2, 0.15, 0.2]}
+
+
+def load_scene_json(path):
+    """scene.json (train.rs:238-262: activated colours / ambient, softplus radii without the +0.01,
+    raw light_dir) as the activated scene the renderer sees (radius + 0.01, scene.rs:43)."""
+    d = json.load(open(path))
+    c = np.asarray(d["centers"], np.float32).reshape(-1, 3)
+    return {"centers": c, "colors": np.asarray(d["colors"], np.float32).reshape(-1, 3),
+            "radius": (np.asarray(d["radii"], np.float32) + np.float32(0.01)).astype(np.float32),
+            "light_dir": np.asarray(d["light_dir"], np.float32).reshape(3),
+            "ambient": np.asarray(d["ambient_intensity"], np.float32).reshape(1)}
+
+
+def load_target_files(cameras_json, entries, W, H):
+    """The target PNGs cameras.json names (util.rs:21-33 linear RGB), resolved as rm_train does:
+    as given, next to the json, or by file name next to the json."""
+    from burn_raymarching_amd import host
+    base = os.path.dirname(os.path.abspath(cameras_json))
+    out = []
+    for e in entries:
+        f = e["file"]
+        for cand in (f, os.path.join(base, f), os.path.join(base, os.path.basename(f))):
+            if os.path.exists(cand):
+                break
+        img = host.image_load(cand)
+        if img.shape[0] != W * H:
+            raise SystemExit(f"{cand} has {img.shape[0]} pixels, expected {W}x{H}")
+        out.append(img)
+    return np.stack(out)
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -234,6 +279,9 @@ def main():
     from burn_raymarching_amd import render as rmr
     from burn_raymarching_amd.parallel import Shard, ViewShardedStep
 
+    start_scene = load_scene_json(args.scene_json) if args.scene_json else None
+    if start_scene is not None:
+        args.spheres = int(start_scene["centers"].shape[0])
     W, H, M, S, K = args.width, args.height, args.spheres, args.march_steps, args.smooth_k
     strong = args.global_views is not None
     if not strong and not 1 <= args.views_per_gpu <= native.RM_MAX_VIEWS_PER_CALL:
@@ -252,17 +300,33 @@ def main():
     # ---- synthetic scene, targets, optimizer --------------------------------------------
     rr = tuple(args.radius_range) if args.radius_range else (
         (0.03, 0.12) if M <= 256 else ((0.02, 0.06) if M <= 1024 else (0.01, 0.04)))
-    sc0 = rmm.synthetic_scene(M, seed=0, radius_range=rr)
+    sc0 = start_scene if start_scene is not None else rmm.synthetic_scene(M, seed=0, radius_range=rr)
     sc1 = rmm.synthetic_scene(M, seed=1, radius_range=rr)
-    ring = max(args.ring, shard.views_total)
+    if args.cameras:  # the reference's poses (data/cameras.json) instead of the synthetic ring
+        cam_entries = json.load(open(args.cameras))
+        cams = [(c["origin"], c["target"], c["fov"]) for c in cam_entries]
+        ring = len(cams)
+        if shard.count() > ring:
+            raise SystemExit(f"{shard.count()} views per rank per step but {args.cameras} holds {ring} cameras")
+    else:
+        cam_entries = None
+        ring = max(args.ring, shard.views_total)
+        cams = [rmm.ring_cameras(ring)[a] for a in ring_order(ring, args.ring_order)]
     shard.ring = ring
-    cams = [rmm.ring_cameras(ring)[a] for a in ring_order(ring, args.ring_order)]
-    tgt_scene = rmm.scene_tensors(sc1)
     targets = torch.empty((ring, npix, 3), device="cuda")
-    for v0 in range(0, ring, native.RM_MAX_VIEWS_PER_CALL):
-        chunk = cams[v0:v0 + native.RM_MAX_VIEWS_PER_CALL]
-        targets[v0:v0 + len(chunk)] = rmr.render_diff_camera(chunk, W, H, tgt_scene, K, S).view(len(chunk), npix, 3)
-    model = rmm.SceneModel.from_activated(sc0["centers"], sc0["colors"], sc0["radius"], sc0["light_dir"],
+    if args.targets == "files":
+        targets.copy_(torch.from_numpy(load_target_files(args.cameras, cam_entries, W, H)).view(ring, npix, 3))
+    else:
+        for v0 in range(0, ring, native.RM_MAX_VIEWS_PER_CALL):
+            chunk = cams[v0:v0 + native.RM_MAX_VIEWS_PER_CALL]
+            if args.targets == "dango":  # generate.rs:29-40 through the renderer.rs kernel
+                t = [torch.tensor(DANGO[k], device="cuda") for k in ("centers", "colors", "radius")]
+                img = rmr.render_camera(chunk, W, H, *t)
+            else:
+                img = rmr.render_diff_camera(chunk, W, H, rmm.scene_tensors(sc1), K, S)
+            targets[v0:v0 + len(chunk)] = img.view(len(chunk), npix, 3)
+    model = rmm.SceneModel.from_activated(sc0["centers"], np.clip(sc0["colors"], 1e-6, 1 - 1e-6), sc0["radius"],
+                                          sc0["light_dir"],
                                           sc0["ambient"], color_dtype=args.color_dtype)
     opt = rmm.Adam(model, weight_decay=1e-5, with_penalties=True)
     march = native.march_params(S, K, skip_escaped=args.skip_escaped == "on")
@@ -356,6 +420,7 @@ def main():
     for j, i in enumerate(range(args.warmup, total_steps)):
         timed = args.kernel_timing == "on" and j % every == 0
         ctx.timing(timed)
+        dp.time_allreduce = timed
         timed_steps += timed
         if ev[j] is not None:
             ev[j][0].record()
@@ -363,6 +428,7 @@ def main():
         if ev[j] is not None:
             ev[j][1].record()
     host_s = time.perf_counter() - t0  # host time to submit the K steps (before the final sync)
+    dp.time_allreduce = False
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -384,6 +450,7 @@ def main():
 
     st = {"blocks": 0, "blocks_skipped": 0, "waves": 0, "waves_exited": 0, "steps_saved": 0}
     canon_ms = None
+    exit_off_s = None
     if args.aux_steps > 0:
         ctx.stats(True)
         ctx.collect_stats(reset=True)
@@ -398,12 +465,40 @@ def main():
             cms, cl = ctx.collect_timing(reset=True)
             canon_steps = sum(1 for j in range(args.steps) if j % every == 0 and j > 0)
             canon_ms = cms / canon_steps if cl and canon_steps else None  # per step (a step may be several launches)
+            # the whole step with the exit off (full work per ray), no events inside: value_exit_off
+            restore()
+            if dist is not None:
+                dist.barrier()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for i in range(args.warmup, total_steps):
+                step(i)
+            torch.cuda.synchronize()
+            if dist is not None:
+                dist.barrier()
+            exit_off_s = time.perf_counter() - t1
             march.flags &= ~native.RM_MARCH_NO_EARLY_EXIT
 
+    ranks_info = None
+    kern_rank_ms = kern_ms / max(timed_steps, 1)  # this rank's train-kernel time per step
     if dist is not None:
-        t = torch.tensor([elapsed, kern_ms, canon_ms or 0.0], device="cuda", dtype=torch.float64)
+        # per-rank train-kernel and all-reduce times (sampled steps), before the max over ranks
+        ar_ms = dp.collect_allreduce_ms()
+        mine = torch.tensor([kern_rank_ms, ar_ms if ar_ms is not None else -1.0], device="cuda", dtype=torch.float64)
+        every_rank = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(every_rank, mine)
+        per = torch.stack(every_rank).cpu().numpy()
+        ranks_info = {"train_kernel_ms_per_step": [round(float(x), 4) for x in per[:, 0]],
+                      "train_kernel_ms_min_max": [round(float(per[:, 0].min()), 4), round(float(per[:, 0].max()), 4)],
+                      "allreduce_ms_per_step": [round(float(x), 4) for x in per[:, 1]],
+                      "allreduce_ms_min_max": [round(float(per[:, 1].min()), 4), round(float(per[:, 1].max()), 4)],
+                      "allreduce_note": "hipEvents on the compute stream around dist.all_reduce of the 7M+5-float "
+                                        "[gradient | loss] on every timed step the kernel is timed on: the collective "
+                                        "plus the wait for the slowest rank's train step",
+                      "allreduce_bytes": 4 * (rmm.packed_size(M) + 1)}
+        t = torch.tensor([elapsed, kern_ms, canon_ms or 0.0, exit_off_s or 0.0], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms, canon_ms = float(t[0]), float(t[1]), (float(t[2]) or None)
+        elapsed, kern_ms, canon_ms, exit_off_s = float(t[0]), float(t[1]), (float(t[2]) or None), (float(t[3]) or None)
         dist.all_reduce(step_ms, op=dist.ReduceOp.MAX)
     step_ms = step_ms.cpu().numpy()
     med_ms = float(np.median(step_ms))
@@ -436,7 +531,8 @@ def main():
     achieved_tf = (flop_per_ray * rays_per_rank * executed_frac / (kern_step_ms * 1e-3) / 1e12
                    if have_stats else None)
     key = (f"{W}x{H}_M{M}_S{S}_V{vpg}" + ("_c16" if args.color_dtype == "f16" else "")
-           + (f"_k{K:g}" if K != 32.0 else ""))
+           + (f"_k{K:g}" if K != 32.0 else "") + ("_cj" if args.cameras else "")
+           + ("_grown" if args.scene_json else ""))
     # per step (the step's launches together), like `achieved`; per launch where no per-step
     # summary exists for this workload
     traffic, traffic_src = _latest_profile("r*_pmc_traffic.json", key, "train_kernel_bytes_per_step")
@@ -450,11 +546,17 @@ def main():
     slab_bytes = (rays_per_rank + 255) // 256 * (mpad * 8 + 8) * 4  # partial-gradient slabs, if all written
     canonical = None
     if canon_ms:
-        ach = flop_per_ray * rays_per_rank / (canon_ms * 1e-3) / 1e12
+        # with the exit off every ray runs S march + 5 post-march sweeps (reconnect, shade, the normal
+        # as the one gradient sweep the kernel runs, 2 backward): 16*(S+5)*M FLOP; the reference's
+        # 16*(S+10)*M credits its six normal taps, which this kernel does not run
+        ach = FLOP_PER_EVAL * (S + 5) * M * rays_per_rank / (canon_ms * 1e-3) / 1e12
+        ach_ref = flop_per_ray * rays_per_rank / (canon_ms * 1e-3) / 1e12
         canonical = {"kernel_ms": round(canon_ms, 4), "achieved": round(ach, 3),
-                     "frac": round(ach / PEAK_FP32_TFLOPS, 4),
-                     "note": "full 16*(S+10)*M FLOP per ray over the kernel time of the timed steps replayed "
-                             "untimed with the early exit off"}
+                     "frac": round(ach / PEAK_FP32_TFLOPS, 4), "flop_per_ray": FLOP_PER_EVAL * (S + 5) * M,
+                     "frac_reference_taps": round(ach_ref / PEAK_FP32_TFLOPS, 4),
+                     "note": "exit off: 16*(S+5)*M FLOP per ray (the sweeps the kernel runs) over the kernel time of "
+                             "the timed steps replayed untimed with the early exit off; frac_reference_taps credits "
+                             "the reference's 16*(S+10)*M (six normal taps)"}
     roofline = None if launches == 0 else {
         "bound": "valu",
         "kernel": "rm_ray_kernel<train,camera>",
@@ -501,7 +603,10 @@ def main():
             "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (seeded scene + targets rendered by the forward kernel)",
+            "data": ("synthetic (seeded scene + targets rendered by the forward kernel)" if args.targets == "synthetic"
+                     and not args.scene_json and not args.cameras else
+                     f"start scene {'file ' + os.path.basename(args.scene_json) if args.scene_json else 'synthetic seed 0'}"
+                     f", targets {args.targets}, poses {'cameras.json' if args.cameras else 'synthetic ring'}"),
             "config": {"workload": (f"train step fwd+bwd, {shard.views_total} {W}x{H} views per step over all GPUs"
                                     if strong else f"train step fwd+bwd, {vpg} {W}x{H} view(s) per GPU")
                                    + f", {M} spheres, {S} march steps, k={K:g}, camera mode, Adam"
@@ -511,12 +616,19 @@ def main():
                        "streams": nstreams,
                        "ring": ring, "ring_order": args.ring_order, "rays_per_step": rays_global, "radius_range": list(rr),
                        "color_storage": args.color_dtype, "sdf_dtype": "f32",
+                       "cameras": args.cameras and os.path.relpath(os.path.abspath(args.cameras), ROOT),
+                       "targets": args.targets,
+                       "start_scene": args.scene_json and os.path.relpath(os.path.abspath(args.scene_json), ROOT),
                        "parallelism": f"views-dp{world}" + ("" if backend == "nccl" else f" ({backend} rehearsal)")},
             "value_median": round(rays_global / (med_ms * 1e-3) / 1e6, 3),
+            "value_exit_off": None if not exit_off_s else round(rays_global * args.steps / exit_off_s / 1e6, 3),
+            "value_exit_off_note": "the same steps replayed untimed-by-events with the exact early exit off (every "
+                                   "ray does the full march): whole-step Mrays/s independent of how many rays escape",
             "ms_per_step_median": round(med_ms, 4),
             "host_submit_ms_per_step": round(host_s / args.steps * 1e3, 4),
             "ms_per_step_min_max": [round(float(step_ms.min()), 4), round(float(step_ms.max()), 4)],
             "roofline": roofline,
+            "ranks": ranks_info,
             "cpu_baseline": cpu,
             "escape_skip": {"enabled": args.skip_escaped == "on", "blocks": blocks_run,
                             "blocks_skipped": blocks_skipped, "skipped_frac": round(skipped_frac, 4)},

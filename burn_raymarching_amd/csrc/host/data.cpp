@@ -178,7 +178,14 @@ void rmh_initial_model(float* raw) {
 
 int rmh_prune_and_split(const float* raw, int32_t M, const float* init_centers, int32_t stage, int32_t stages,
                         rmh_rng* rng, float* out, int32_t* out_M) {
-  if (!raw || !init_centers || !rng || !out || !out_M || M < 1 || stage < 0 || stages < 1)
+  return rmh_prune_and_split_ex(raw, M, init_centers, stage, stages, 1.0f, 0.05f, 0, rng, out, out_M);
+}
+
+int rmh_prune_and_split_ex(const float* raw, int32_t M, const float* init_centers, int32_t stage, int32_t stages,
+                           float split_scale, float split_move, int32_t max_spheres, rmh_rng* rng, float* out,
+                           int32_t* out_M) {
+  if (!raw || !init_centers || !rng || !out || !out_M || M < 1 || stage < 0 || stages < 1 || !(split_scale >= 0.0f) ||
+      !(split_move >= 0.0f) || max_spheres < 0)
     return fail(RMH_ERR_INVALID_ARG, "bad prune_and_split arguments");
   const float* cen = raw;
   const float* col = raw + 3 * M;
@@ -202,8 +209,11 @@ int rmh_prune_and_split(const float* raw, int32_t M, const float* init_centers, 
       nr.push_back(rawr);
     };
     if (stage < stages - 1) {
-      const float split_threshold = 0.25f * std::pow(0.65f, (float)stage);  // training.rs:185
-      if (r > split_threshold && move_dist_sq > 0.05f * 0.05f) {
+      // training.rs:185-188 (split_scale 1, split_move 0.05: the reference's f32 values exactly)
+      const float split_threshold = split_scale * (0.25f * std::pow(0.65f, (float)stage));
+      // the cap (growth runs): the two children plus every later sphere kept must still fit
+      const bool fits = max_spheres == 0 || (int64_t)nr.size() + 2 + (M - 1 - i) <= (int64_t)max_spheres;
+      if (r > split_threshold && move_dist_sq > split_move * split_move && fits) {
         // training.rs:192-222: random unit direction, children at +-r/2 with radius 0.8 r
         const float z = rmh_rng_uniform(rng, -1.0f, 1.0f);
         const float theta = rmh_rng_uniform(rng, 0.0f, 6.2831855f);

@@ -46,8 +46,10 @@ struct DevBuf {
   int32_t* i() const { return (int32_t*)p; }
 };
 
-// A rank that leaves rmh_train with an error aborts the collective (rmh_collective.abort), so the
-// other ranks' pending all-reduce / broadcast fail instead of waiting for it forever.
+// A rank that leaves rmh_train with an error releases its side of the collectives
+// (rmh_collective.abort: the RCCL one aborts its communicator). The other ranks learn of it through
+// their own watchdog (rmh_collective.wait at every synchronisation point of the driver) or from
+// the launcher, which ends the remaining ranks when one fails.
 struct AbortOnError {
   const rmh_collective* comm = nullptr;
   bool done = false;
@@ -71,6 +73,42 @@ struct Gpu {
     return RMH_OK;
   }
 };
+
+// Waits for the driver's stream: through the collective's watchdog when collectives may be in
+// flight (a dead peer then ends in an error instead of a hang), else hipStreamSynchronize.
+int sync_stream(const Gpu& g, const rmh_collective* comm) {
+  if (comm && comm->wait) {
+    const int rc = comm->wait(comm->state, g.stream);
+    if (rc != RMH_OK) {
+      const std::string why = rmh_last_error();
+      return fail(rc, "waiting for the stream: %s", why.c_str());
+    }
+    return RMH_OK;
+  }
+  HIPCHK(hipStreamSynchronize(g.stream));
+  return RMH_OK;
+}
+
+// IEEE binary16, round to nearest even (the conversion torch's .half() and the optimizer's
+// colors_f16_out use), for the initial fp16 colours of a stage.
+uint16_t f32_to_f16(float x) {
+  uint32_t u;
+  std::memcpy(&u, &x, 4);
+  const uint32_t sign = (u >> 16) & 0x8000u;
+  const uint32_t ax = u & 0x7fffffffu;
+  if (ax >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (ax > 0x7f800000u ? 0x200u : 0u));  // inf / nan
+  if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);  // rounds past 65504: inf
+  if (ax < 0x38800000u) {  // subnormal half (or zero): scale by 2^24 and round
+    float a;
+    std::memcpy(&a, &ax, 4);
+    return (uint16_t)(sign | (uint32_t)std::nearbyint(a * 16777216.0f));
+  }
+  const uint32_t mant = ax & 0x7fffffu;
+  uint32_t h = ((ax >> 23) - 112u) << 10 | (mant >> 13);
+  const uint32_t rest = mant & 0x1fffu;
+  if (rest > 0x1000u || (rest == 0x1000u && (h & 1u))) ++h;  // carries into the exponent correctly
+  return (uint16_t)(sign | h);
+}
 
 bool file_exists(const std::string& p) {
   FILE* f = std::fopen(p.c_str(), "rb");
@@ -100,13 +138,17 @@ void camera_struct(rm_camera& c, const float eye[3], const float target[3], floa
 
 // save_tiled_preview (train.rs:335-366): render_diff at k = 32 of the activated packed model,
 // whole image in one camera-mode launch (the reference chunks 4096 rays only to save VRAM).
-int preview_packed(Gpu& g, const float* act_dev, int32_t M, int32_t W, int32_t H, int32_t steps,
-                   const std::string& path) {
+int preview_packed(Gpu& g, const float* act_dev, const uint16_t* colors_f16, int32_t M, int32_t W, int32_t H,
+                   int32_t steps, const std::string& path) {
   rm_scene sc;
   rm_scene_from_packed(act_dev, M, &sc);
   rm_march m;
   rm_march_default(&m);
   m.steps = steps;
+  if (colors_f16) {  // an fp16-colour model previews with the colours it trains with
+    sc.colors = (const float*)colors_f16;
+    m.flags |= RM_MARCH_COLOR_F16;
+  }
   m.smooth_k = 32.0f;
   rm_camera cam;
   const float eye[3] = {0.0f, 0.0f, -2.5f}, tgt[3] = {0.0f, 0.0f, 0.0f};  // train.rs:37-44
@@ -152,13 +194,16 @@ void rmh_train_config_default(rmh_train_config* c) {
   c->previews = 1;
   c->seed = 0;
   c->device = 0;
+  c->split_scale = 1.0f;   // training.rs:185
+  c->split_move = 0.05f;   // training.rs:188
 }
 
 int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_out, int32_t raw_capacity) {
   if (!cfg || !cfg->cameras_json) return fail(RMH_ERR_INVALID_ARG, "NULL config");
   if (cfg->width < 1 || cfg->height < 1 || cfg->stages < 1 || cfg->steps_per_stage < 1 || cfg->batch < 1 ||
-      cfg->march_steps < 1)
+      cfg->march_steps < 1 || !(cfg->split_scale >= 0.0f) || !(cfg->split_move >= 0.0f) || cfg->max_spheres < 0)
     return fail(RMH_ERR_INVALID_ARG, "bad training configuration");
+  const bool f16 = cfg->color_f16 != 0;
   const int32_t W = cfg->width, H = cfg->height;
   const rmh_collective* comm = cfg->comm;
   const int32_t world = comm ? comm->world : 1, rank = comm ? comm->rank : 0;
@@ -240,12 +285,13 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
   rm_march march;
   rm_march_default(&march);
   march.steps = cfg->march_steps;
+  if (f16) march.flags |= RM_MARCH_COLOR_F16;
   if (verbose) std::printf("Start Multi-Stage Optimization...\n");
 
   for (int32_t stage = 0; stage < cfg->stages; ++stage) {
     if (verbose) std::printf("=== Stage %d/%d (N = %d) ===\n", stage + 1, cfg->stages, M);
     const size_t np = 7 * (size_t)M + 4;
-    DevBuf d_raw, d_act, d_grad, d_m, d_v;
+    DevBuf d_raw, d_act, d_grad, d_m, d_v, d_col_h;
     HIPCHK(d_raw.alloc(sizeof(float) * np));
     HIPCHK(d_act.alloc(sizeof(float) * np));
     // [packed gradient (np) | loss sum | penalty]: the first np + 1 floats are the one all-reduce
@@ -257,15 +303,28 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
     HIPCHK(hipMemsetAsync(d_m.p, 0, d_m.bytes, g.stream));  // Adam re-created per stage (train.rs:160)
     HIPCHK(hipMemsetAsync(d_v.p, 0, d_v.bytes, g.stream));
     RMCHK(g.ctx, rm_scene_activate(g.ctx, d_raw.f(), M, d_act.f()));
+    uint16_t* col_h = nullptr;  // fp16-colour models: the activated colours the renders read
+    if (f16) {
+      std::vector<float> col(3 * (size_t)M);
+      std::vector<uint16_t> half(3 * (size_t)M);
+      HIPCHK(hipMemcpyAsync(col.data(), d_act.f() + 3 * M, sizeof(float) * col.size(), hipMemcpyDeviceToHost,
+                            g.stream));
+      HIPCHK(hipStreamSynchronize(g.stream));
+      for (size_t i = 0; i < col.size(); ++i) half[i] = f32_to_f16(col[i]);
+      HIPCHK(d_col_h.alloc(sizeof(uint16_t) * half.size()));
+      HIPCHK(hipMemcpyAsync(d_col_h.p, half.data(), d_col_h.bytes, hipMemcpyHostToDevice, g.stream));
+      col_h = (uint16_t*)d_col_h.p;
+    }
     RMCHK(g.ctx, rm_reserve(g.ctx, B, M));
     const std::vector<float> init_centers(raw.begin(), raw.begin() + 3 * M);
     const double base_lr = (double)cfg->base_lr * std::pow(0.6, stage);  // train.rs:166
     rm_scene sc;
     rm_scene_from_packed(d_act.f(), M, &sc);
+    if (f16) sc.colors = (const float*)col_h;
     rm_grads gr;
     rm_grads_from_packed(d_grad.f(), M, &gr);
 
-    HIPCHK(hipStreamSynchronize(g.stream));
+    if ((rc = sync_stream(g, comm)) != RMH_OK) return rc;
     const auto t0 = std::chrono::steady_clock::now();
     for (int32_t step = 1; step <= cfg->steps_per_stage; ++step) {
       const float global_step = (float)(stage * cfg->steps_per_stage + step);
@@ -288,7 +347,7 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
       const double lr = step > cfg->steps_per_stage / 2 ? base_lr * 0.2 : base_lr;  // train.rs:193-197
       const bool last = stage == cfg->stages - 1 && step == cfg->steps_per_stage;
       const bool read_loss = (verbose && step % cfg->log_every == 0) || last;
-      if (!comm) {
+      if (!comm && !f16) {
         // one process, no collective: draw + render + backward + optimizer in one call (one
         // launch for the small models of the schedule; the penalty share only on reporting steps)
         RMCHK(g.ctx, rm_train_iteration(g.ctx, d_org.f(), d_dir.f(), d_tgt.f(), P, d_fg.i(), n_fg_list, n_uni, n_boost,
@@ -301,32 +360,39 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
                                      nullptr));
         RMCHK(g.ctx, rm_train_step(g.ctx, b_org.f(), b_dir.f(), b_tgt.f(), n, progress, inv_count, &sc, &march, &gr,
                                    d_loss, nullptr, 0));
-        if ((rc = comm->all_reduce_sum(comm->state, d_grad.f(), (int64_t)np + 1, g.stream)) != RMH_OK)
+        if (comm && (rc = comm->all_reduce_sum(comm->state, d_grad.f(), (int64_t)np + 1, g.stream)) != RMH_OK)
           return fail(rc, "all-reduce of the gradient (stage %d, step %d): %s", stage, step, rmh_last_error());
         // the penalty share of the loss costs a summation launch: only on the steps that report it
-        RMCHK(g.ctx, rm_optimizer_step(g.ctx, d_raw.f(), d_grad.f(), d_m.f(), d_v.f(), M, step, (float)lr,
-                                       cfg->weight_decay, 1, read_loss ? d_loss + 1 : nullptr, d_act.f()));
+        if (f16)
+          RMCHK(g.ctx, rm_optimizer_step_f16(g.ctx, d_raw.f(), d_grad.f(), d_m.f(), d_v.f(), M, step, (float)lr,
+                                             cfg->weight_decay, 1, read_loss ? d_loss + 1 : nullptr, d_act.f(), col_h));
+        else
+          RMCHK(g.ctx, rm_optimizer_step(g.ctx, d_raw.f(), d_grad.f(), d_m.f(), d_v.f(), M, step, (float)lr,
+                                         cfg->weight_decay, 1, read_loss ? d_loss + 1 : nullptr, d_act.f()));
       }
       ++steps_done;
       if (read_loss) {
         float s[2];
-        HIPCHK(hipMemcpyAsync(s, d_loss, sizeof s, hipMemcpyDeviceToHost, g.stream));
-        HIPCHK(hipStreamSynchronize(g.stream));
+        // drain the stream under the watchdog first: a copy to pageable memory blocks unguarded
+        if ((rc = sync_stream(g, comm)) != RMH_OK) return rc;
+        HIPCHK(hipMemcpy(s, d_loss, sizeof s, hipMemcpyDeviceToHost));
         last_loss = s[0] * inv_count + s[1];  // training.rs:34 + penalties
         if (verbose && step % cfg->log_every == 0)
           std::printf("  Step %d | Loss: %.5f | k: %.1f\n", step, last_loss, march.smooth_k);
       }
     }
-    HIPCHK(hipStreamSynchronize(g.stream));
+    if ((rc = sync_stream(g, comm)) != RMH_OK) return rc;
     seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     HIPCHK(hipMemcpy(raw.data(), d_raw.p, sizeof(float) * np, hipMemcpyDeviceToHost));
+    if (cfg->on_generation) cfg->on_generation(cfg->user, stage, M, raw.data());
 
     if (stage == cfg->stages - 1) {  // train.rs:206-290
       if (lead && !out_dir.empty()) {
         if ((rc = export_scene(raw, M, join_path(out_dir, "scene.json"))) != RMH_OK) return rc;
         if (verbose) std::printf("  => Saved to scene.json (N = %d)\n", M);
         if (cfg->previews &&
-            (rc = preview_packed(g, d_act.f(), M, W, H, cfg->march_steps, join_path(out_dir, "steps/final_1.png"))))
+            (rc = preview_packed(g, d_act.f(), col_h, M, W, H, cfg->march_steps,
+                                 join_path(out_dir, "steps/final_1.png"))))
           return rc;
       }
       break;
@@ -334,15 +400,16 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
     if (lead && cfg->previews && !out_dir.empty()) {
       char name[64];
       std::snprintf(name, sizeof name, "steps/stage_%d.png", stage);
-      if ((rc = preview_packed(g, d_act.f(), M, W, H, cfg->march_steps, join_path(out_dir, name)))) return rc;
+      if ((rc = preview_packed(g, d_act.f(), col_h, M, W, H, cfg->march_steps, join_path(out_dir, name)))) return rc;
     }
     // ---- C. prune & split (train.rs:300-328) ----
     // rank 0 decides the next generation and broadcasts it: its size, then its raw params
     std::vector<float> next(14 * (size_t)M + 4);
     int32_t nextM = 0;
     int split_rc = RMH_OK;
-    if (lead) split_rc = rmh_prune_and_split(raw.data(), M, init_centers.data(), stage, cfg->stages, &rng_split,
-                                             next.data(), &nextM);
+    if (lead)
+      split_rc = rmh_prune_and_split_ex(raw.data(), M, init_centers.data(), stage, cfg->stages, cfg->split_scale,
+                                        cfg->split_move, cfg->max_spheres, &rng_split, next.data(), &nextM);
     if (split_rc != RMH_OK && !comm) return split_rc;
     if (comm) {  // (with one rank too: the RCCL path is the same)
       DevBuf d_next;
@@ -352,8 +419,8 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
       HIPCHK(hipMemcpyAsync(d_next.p, &fm, sizeof fm, hipMemcpyHostToDevice, g.stream));
       if ((rc = comm->broadcast(comm->state, d_next.f(), 1, 0, g.stream)) != RMH_OK)
         return fail(rc, "broadcast of the next size: %s", rmh_last_error());
-      HIPCHK(hipMemcpyAsync(&fm, d_next.p, sizeof fm, hipMemcpyDeviceToHost, g.stream));
-      HIPCHK(hipStreamSynchronize(g.stream));
+      if ((rc = sync_stream(g, comm)) != RMH_OK) return rc;
+      HIPCHK(hipMemcpy(&fm, d_next.p, sizeof fm, hipMemcpyDeviceToHost));
       nextM = (int32_t)fm;
       if (split_rc != RMH_OK) return split_rc;  // rank 0, after telling the others
       if (nextM < 0) return fail(RMH_ERR_GPU, "rank 0 failed in prune_and_split (stage %d)", stage);
@@ -362,8 +429,8 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
       if (lead) HIPCHK(hipMemcpyAsync(d_next.p, next.data(), sizeof(float) * nn, hipMemcpyHostToDevice, g.stream));
       if ((rc = comm->broadcast(comm->state, d_next.f(), (int64_t)nn, 0, g.stream)) != RMH_OK)
         return fail(rc, "broadcast of the next generation: %s", rmh_last_error());
-      HIPCHK(hipMemcpyAsync(next.data(), d_next.p, sizeof(float) * nn, hipMemcpyDeviceToHost, g.stream));
-      HIPCHK(hipStreamSynchronize(g.stream));
+      if ((rc = sync_stream(g, comm)) != RMH_OK) return rc;
+      HIPCHK(hipMemcpy(next.data(), d_next.p, sizeof(float) * nn, hipMemcpyDeviceToHost));
     }
     if (nextM > RM_MAX_SPHERES) return fail(RMH_ERR_INVALID_ARG, "model grew past RM_MAX_SPHERES");
     next.resize(7 * (size_t)nextM + 4);

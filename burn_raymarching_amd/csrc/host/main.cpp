@@ -4,9 +4,15 @@
 //   rm_train train    [--cameras data/cameras.json] [--out .] [--stages 5] [--steps 700]
 //                     [--batch 16384] [--size 256x256] [--march-steps 40] [--seed 0]
 //                     [--log-every 100] [--no-previews] [--device 0] [--ranks N]
+//                     [--split-scale 1] [--split-move 0.05] [--max-spheres 0] [--color-f16]
 //     --ranks N: data-parallel training on N GPUs (devices 0..N-1), one process per GPU over
 //     RCCL: this process forks the N rank processes before anything touches a GPU and waits
-//     for them. (--rank r --world N --comm-file F run one rank of a run launched elsewhere.)
+//     for them. (--rank r --world N --comm-file F [--run-id S] [--comm-timeout SEC] run one rank
+//     of a run launched elsewhere: every rank of the run gets the same F and S.)
+//     --split-scale / --split-move: prune_and_split's split thresholds (rmh_prune_and_split_ex;
+//     0 and 0 split every surviving sphere, for growth runs such as BASELINE configs[4];
+//     --max-spheres caps the next generation, 0 = no cap);
+//     --color-f16: fp16 colour / fp32 SDF.
 //   rm_train generate [--out data] [--prefix data/] [--size 256x256] [--device 0]
 //   rm_train preview  --scene scene.json --png out.png [--size 256x256]
 //                     [--eye 0,0,-2.5] [--target 0,0,0] [--fov 50] [--radius-offset 0.01]
@@ -29,6 +35,8 @@ int usage() {
                "usage: rm_train train|generate|preview [options]\n"
                "  train    --cameras F --out D --stages N --steps N --batch N --size WxH --march-steps N\n"
                "           --seed N --log-every N --no-previews --device N --ranks N\n"
+               "           --split-scale F --split-move F --max-spheres N --color-f16\n"
+               "           --rank R --world N --comm-file F --run-id S --comm-timeout SEC\n"
                "  generate --out D --prefix P --size WxH --device N\n"
                "  preview  --scene F --png F --size WxH --eye x,y,z --target x,y,z --fov F --radius-offset F\n");
   return 2;
@@ -44,10 +52,12 @@ int report(int rc, const char* what) {
 }
 
 // One rank of a data-parallel run: RCCL communicator, rmh_train, rank 0 prints the result.
-int train_rank(rmh_train_config cfg, int rank, int world, const char* comm_file) {
+int train_rank(rmh_train_config cfg, int rank, int world, const char* comm_file, const char* run_id,
+               double comm_timeout) {
   rmh_collective comm;
   if (world > 1 || rank >= 0) {
-    if (rmh_collective_rccl_create(rank, world, cfg.device, comm_file, 300.0, &comm) != RMH_OK)
+    if (rmh_collective_rccl_create(rank, world, cfg.device, comm_file, run_id, comm_timeout, &comm) !=
+        RMH_OK)
       return report(RMH_ERR_GPU, "train (RCCL)");
     cfg.comm = &comm;
   }
@@ -64,13 +74,15 @@ int train_rank(rmh_train_config cfg, int rank, int world, const char* comm_file)
 // --ranks N: one rank process per GPU (devices 0..N-1), forked before this process touches a
 // GPU (no exec: each child runs its rank directly). Waits for all; when one fails the others
 // are terminated. Returns the first failing exit status (0 if all succeed).
-int launch_ranks(const rmh_train_config& cfg, int n) {
+int launch_ranks(const rmh_train_config& cfg, int n, double comm_timeout) {
   char dir[] = "/tmp/rm_train_XXXXXX";
   if (!mkdtemp(dir)) {
     std::perror("mkdtemp");
     return 1;
   }
   const std::string id_file = std::string(dir) + "/rccl_id";
+  char run_id[64];  // the directory is fresh already; the id makes the file's owner explicit
+  std::snprintf(run_id, sizeof run_id, "rm_train-%d-%s", (int)getpid(), dir + 5);
   std::fflush(nullptr);
   std::vector<pid_t> pids;
   for (int r = 0; r < n; ++r) {
@@ -83,7 +95,7 @@ int launch_ranks(const rmh_train_config& cfg, int n) {
     if (pid == 0) {
       rmh_train_config c = cfg;
       c.device = r;
-      const int code = train_rank(c, r, n, id_file.c_str());
+      const int code = train_rank(c, r, n, id_file.c_str(), run_id, comm_timeout);
       std::fflush(nullptr);
       _exit(code);
     }
@@ -119,10 +131,14 @@ int main(int argc, char** argv) {
     int ranks = 0, rank = -1, world = 1;
     bool device_given = false;
     const char* comm_file = nullptr;
+    const char* run_id = nullptr;
+    double comm_timeout = 300.0;
     for (int i = 2; i < argc; ++i) {
       const std::string a = argv[i];
       if (a == "--no-previews") {
         cfg.previews = 0;
+      } else if (a == "--color-f16") {
+        cfg.color_f16 = 1;
       } else if (!need(i)) {
         return usage();
       } else if (a == "--cameras") {
@@ -154,18 +170,28 @@ int main(int argc, char** argv) {
         world = std::atoi(argv[++i]);
       } else if (a == "--comm-file") {
         comm_file = argv[++i];
+      } else if (a == "--run-id") {
+        run_id = argv[++i];
+      } else if (a == "--comm-timeout") {
+        comm_timeout = std::atof(argv[++i]);
+      } else if (a == "--split-scale") {
+        cfg.split_scale = (float)std::atof(argv[++i]);
+      } else if (a == "--split-move") {
+        cfg.split_move = (float)std::atof(argv[++i]);
+      } else if (a == "--max-spheres") {
+        cfg.max_spheres = std::atoi(argv[++i]);
       } else {
         return usage();
       }
     }
-    if (ranks > 0) return launch_ranks(cfg, ranks);
+    if (ranks > 0) return launch_ranks(cfg, ranks, comm_timeout);
     // one rank of a run launched elsewhere: without --device it takes LOCAL_RANK's device (or
     // its rank's): RCCL refuses two ranks on one device
     if (world > 1 && !device_given) {
       const char* lr = std::getenv("LOCAL_RANK");
       cfg.device = lr ? std::atoi(lr) : rank;
     }
-    return train_rank(cfg, rank, world, comm_file);
+    return train_rank(cfg, rank, world, comm_file, run_id, comm_timeout);
   }
   if (cmd == "generate") {
     const char* out = "data";

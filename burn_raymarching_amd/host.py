@@ -38,13 +38,16 @@ BROADCAST_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, 
 
 
 ABORT_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+WAIT_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p)
+GENERATION_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.POINTER(ctypes.c_float))
 
 
 class RmhCollective(ctypes.Structure):
     """rmh_collective: sum all-reduce and broadcast of fp32 device buffers on the driver's stream,
-    and the (nullable) abort a failing rank calls."""
+    the (nullable) abort a failing rank calls and the (nullable) watchdog wait on the stream."""
     _fields_ = [("state", ctypes.c_void_p), ("rank", ctypes.c_int32), ("world", ctypes.c_int32),
-                ("all_reduce_sum", ALL_REDUCE_FN), ("broadcast", BROADCAST_FN), ("abort", ABORT_FN)]
+                ("all_reduce_sum", ALL_REDUCE_FN), ("broadcast", BROADCAST_FN), ("abort", ABORT_FN),
+                ("wait", WAIT_FN)]
 
 
 class RmhTrainConfig(ctypes.Structure):
@@ -53,7 +56,9 @@ class RmhTrainConfig(ctypes.Structure):
                 ("batch", ctypes.c_int32), ("march_steps", ctypes.c_int32), ("max_smooth", ctypes.c_float),
                 ("base_lr", ctypes.c_float), ("weight_decay", ctypes.c_float), ("log_every", ctypes.c_int32),
                 ("previews", ctypes.c_int32), ("seed", ctypes.c_uint64), ("device", ctypes.c_int32),
-                ("comm", ctypes.POINTER(RmhCollective))]
+                ("comm", ctypes.POINTER(RmhCollective)), ("split_scale", ctypes.c_float),
+                ("split_move", ctypes.c_float), ("max_spheres", ctypes.c_int32), ("color_f16", ctypes.c_int32), ("on_generation", GENERATION_FN),
+                ("user", ctypes.c_void_p)]
 
 
 class RmhTrainResult(ctypes.Structure):
@@ -94,9 +99,13 @@ SIGNATURES = {
     "rmh_dataset_sample_count": (None, [_P, _I32, _F, ctypes.POINTER(_I64), ctypes.POINTER(_I64)]),
     "rmh_dataset_fg": (None, [_P, ctypes.POINTER(_PI32), ctypes.POINTER(_I64)]),
     "rmh_prune_and_split": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, ctypes.POINTER(RmhRng), _P, _PI32]),
+    "rmh_prune_and_split_ex": (ctypes.c_int, [_P, _I32, _P, _I32, _I32, _F, _F, _I32, ctypes.POINTER(RmhRng), _P,
+                                              _PI32]),
     "rmh_initial_model": (None, [_P]),
-    "rmh_collective_rccl_create": (ctypes.c_int, [_I32, _I32, _I32, _S, ctypes.c_double,
+    "rmh_collective_rccl_create": (ctypes.c_int, [_I32, _I32, _I32, _S, _S, ctypes.c_double,
                                                   ctypes.POINTER(RmhCollective)]),
+    "rmh_rendezvous_publish": (ctypes.c_int, [_S, _S, _P, _I64]),
+    "rmh_rendezvous_read": (ctypes.c_int, [_S, _S, _P, _I64, ctypes.c_double]),
     "rmh_collective_rccl_destroy": (None, [ctypes.POINTER(RmhCollective)]),
     "rmh_train_config_default": (None, [ctypes.POINTER(RmhTrainConfig)]),
     "rmh_train": (ctypes.c_int, [ctypes.POINTER(RmhTrainConfig), ctypes.POINTER(RmhTrainResult), _P, _I32]),
@@ -305,7 +314,10 @@ class Dataset:
     __del__ = close
 
 
-def prune_and_split(raw_packed, num_spheres, init_centers, stage, stages, rng: Rng):
+def prune_and_split(raw_packed, num_spheres, init_centers, stage, stages, rng: Rng, split_scale=None,
+                    split_move=None, max_spheres=None):
+    """training.rs:87-238; split_scale / split_move / max_spheres (rmh_prune_and_split_ex) default
+    to the reference rule (1, 0.05, no cap)."""
     raw = _f32c(raw_packed).reshape(-1)
     if raw.size != 7 * num_spheres + 4:
         raise ValueError("raw_packed must hold 7M+4 floats")
@@ -314,8 +326,14 @@ def prune_and_split(raw_packed, num_spheres, init_centers, stage, stages, rng: R
         raise ValueError("init_centers must be [M, 3]")
     out = np.empty(14 * num_spheres + 4, np.float32)
     m = _I32()
-    _check(lib().rmh_prune_and_split(_p(raw), num_spheres, _p(init), stage, stages, ctypes.byref(rng.s), _p(out),
-                                     ctypes.byref(m)), "rmh_prune_and_split")
+    if split_scale is None and split_move is None and max_spheres is None:
+        _check(lib().rmh_prune_and_split(_p(raw), num_spheres, _p(init), stage, stages, ctypes.byref(rng.s), _p(out),
+                                         ctypes.byref(m)), "rmh_prune_and_split")
+    else:
+        _check(lib().rmh_prune_and_split_ex(_p(raw), num_spheres, _p(init), stage, stages,
+                                            1.0 if split_scale is None else split_scale,
+                                            0.05 if split_move is None else split_move, max_spheres or 0,
+                                            ctypes.byref(rng.s), _p(out), ctypes.byref(m)), "rmh_prune_and_split_ex")
     return out[:7 * m.value + 4].copy(), m.value
 
 
@@ -336,11 +354,12 @@ def train_config(**kw) -> RmhTrainConfig:
     return cfg
 
 
-def collective(rank: int, world: int, all_reduce_sum, broadcast, abort=None) -> RmhCollective:
+def collective(rank: int, world: int, all_reduce_sum, broadcast, abort=None, wait=None) -> RmhCollective:
     """An rmh_collective over Python callables all_reduce_sum(dev_ptr, count, stream) and
-    broadcast(dev_ptr, count, root, stream) (each returns None or raises), and abort() (optional:
-    called by a rank that fails after the collectives began). The struct keeps the callbacks
-    alive; keep it alive while rmh_train runs."""
+    broadcast(dev_ptr, count, root, stream) (each returns None or raises), abort() (optional:
+    called by a rank that fails after the collectives began) and wait(stream) (optional: the
+    driver's stream waits; raise to fail the run). The struct keeps the callbacks alive; keep it
+    alive while rmh_train runs."""
     def ar(_state, buf, count, stream):
         try:
             all_reduce_sum(buf, count, stream)
@@ -360,18 +379,50 @@ def collective(rank: int, world: int, all_reduce_sum, broadcast, abort=None) -> 
             abort()
         except Exception as e:  # noqa: BLE001
             print(f"abort failed: {e!r}")
+    def wt(_state, stream):
+        try:
+            wait(stream)
+            return RMH_OK
+        except Exception as e:  # noqa: BLE001
+            print(f"wait failed: {e!r}")
+            return 4
     c = RmhCollective(None, rank, world, ALL_REDUCE_FN(ar), BROADCAST_FN(bc),
-                      ABORT_FN(ab) if abort is not None else ABORT_FN())
-    c._keep = (c.all_reduce_sum, c.broadcast, c.abort)
+                      ABORT_FN(ab) if abort is not None else ABORT_FN(),
+                      WAIT_FN(wt) if wait is not None else WAIT_FN())
+    c._keep = (c.all_reduce_sum, c.broadcast, c.abort, c.wait)
     return c
 
 
-def rccl_collective(rank: int, world: int, device: int, id_path: str | None, timeout_s: float = 300.0):
+def rccl_collective(rank: int, world: int, device: int, id_path: str | None, timeout_s: float = 300.0,
+                    run_id: str | None = None):
     """rmh_collective_rccl_create (RCCL over xGMI, one process per GPU)."""
     c = RmhCollective()
     _check(lib().rmh_collective_rccl_create(rank, world, device, None if id_path is None else _b(id_path),
-                                            float(timeout_s), ctypes.byref(c)), "rmh_collective_rccl_create")
+                                            None if run_id is None else run_id.encode(), float(timeout_s),
+                                            ctypes.byref(c)), "rmh_collective_rccl_create")
     return c
+
+
+def rendezvous_publish(path, run_id: str | None, blob: bytes) -> None:
+    buf = ctypes.create_string_buffer(blob, len(blob))
+    _check(lib().rmh_rendezvous_publish(_b(path), None if run_id is None else run_id.encode(), buf, len(blob)),
+           "rmh_rendezvous_publish")
+
+
+def rendezvous_read(path, run_id: str | None, size: int, timeout_s: float) -> bytes:
+    buf = ctypes.create_string_buffer(size)
+    _check(lib().rmh_rendezvous_read(_b(path), None if run_id is None else run_id.encode(), buf, size,
+                                     float(timeout_s)), "rmh_rendezvous_read")
+    return buf.raw[:size]
+
+
+def on_generation(cfg: RmhTrainConfig, fn) -> None:
+    """Set cfg.on_generation to call fn(stage, num_spheres, raw_packed_copy) after each stage's
+    training (every rank); the config keeps the callback alive."""
+    def cb(_user, stage, m, raw):
+        fn(stage, m, np.ctypeslib.as_array(raw, shape=(7 * m + 4,)).copy())
+    cfg._gen_cb = GENERATION_FN(cb)
+    cfg.on_generation = cfg._gen_cb
 
 
 def train(cfg: RmhTrainConfig, max_spheres: int = 65536):

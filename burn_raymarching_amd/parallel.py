@@ -78,15 +78,35 @@ class ViewShardedStep:
         self.step_fn = step_fn
         self.optim_fn = optim_fn
         self.group = group
+        # time_allreduce: hipEvents on the compute stream around the all-reduce of the next steps
+        # (the collective plus the wait for the slowest rank), read by collect_allreduce_ms()
+        self.time_allreduce = False
+        self._ar_events = []
 
     def __call__(self, step: int) -> None:
         views = self.shard.views(step)
         self.step_fn(views, self.inv_count, self.grads, self.loss)
         if self.shard.world > 1:
             import torch.distributed as dist
+            if self.time_allreduce:
+                ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                ev[0].record()
             dist.all_reduce(self.buf, group=self.group)
+            if self.time_allreduce:
+                ev[1].record()
+                self._ar_events.append(ev)
         if self.optim_fn is not None:
             self.optim_fn(self.grads)
+
+    def collect_allreduce_ms(self, reset: bool = True):
+        """Mean ms per timed all-reduce since the last reset (None if none was timed)."""
+        if not self._ar_events:
+            return None
+        torch.cuda.synchronize()
+        ms = [a.elapsed_time(b) for a, b in self._ar_events]
+        if reset:
+            self._ar_events = []
+        return sum(ms) / len(ms)
 
     def mean_loss(self) -> float:
         """Reconstruction loss (training.rs:34 mean) of the last step, over all ranks."""

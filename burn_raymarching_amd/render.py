@@ -238,7 +238,7 @@ def train_step_camera(cams, width, height, targets, scene: Scene, smooth_k, prog
     to run on (default: the one of torch's current stream)."""
     cams = list(cams)
     if not 1 <= len(cams) <= native.RM_MAX_VIEWS_PER_CALL:
-        raise ValueError("1..16 views per call")
+        raise ValueError(f"1..{native.RM_MAX_VIEWS_PER_CALL} views per call")
     n = len(cams) * width * height
     targets = _f32(targets, (n, 3), "targets")
     if inv_count is None:
@@ -314,7 +314,7 @@ def render_camera(cams, width, height, centers, colors, radius):
     """renderer.rs:4-80 with in-kernel camera rays: out [V*H*W, 3] (generate.rs:88-104)."""
     cams = list(cams)
     if not 1 <= len(cams) <= native.RM_MAX_VIEWS_PER_CALL:
-        raise ValueError("1..16 views per call")
+        raise ValueError(f"1..{native.RM_MAX_VIEWS_PER_CALL} views per call")
     m = centers.shape[0]
     centers = _f32(centers, (m, 3), "centers")
     colors = _f32(colors, (m, 3), "colors")

@@ -114,6 +114,18 @@ void rmh_dataset_fg(const rmh_dataset* ds, const int32_t** fg, int64_t* num_fg);
  * Returns RMH_ERR_INVALID_ARG if every sphere was pruned. */
 int rmh_prune_and_split(const float* raw_packed, int32_t num_spheres, const float* init_centers, int32_t stage,
                         int32_t stages, rmh_rng* rng, float* out_packed, int32_t* out_num_spheres);
+/* rmh_prune_and_split with the split rule's thresholds as knobs (growth runs such as
+ * BASELINE configs[4], "4096 spheres after adaptive split/prune"): a sphere splits when
+ * r > split_scale * 0.25 * 0.65^stage and its squared move exceeds split_move^2
+ * (training.rs:185-188), and -- with max_spheres > 0 -- when the next generation then still fits
+ * max_spheres counting every later sphere as kept (spheres are visited in order; a sphere that
+ * would not fit is kept unsplit). split_scale = 1, split_move = 0.05, max_spheres = 0 is the
+ * reference rule (exactly rmh_prune_and_split); split_scale = 0, split_move = 0 splits every
+ * sphere that survives pruning. The pruning rules and the children (training.rs:167-222) are
+ * unchanged. */
+int rmh_prune_and_split_ex(const float* raw_packed, int32_t num_spheres, const float* init_centers, int32_t stage,
+                           int32_t stages, float split_scale, float split_move, int32_t max_spheres, rmh_rng* rng,
+                           float* out_packed, int32_t* out_num_spheres);
 /* The initial 7-sphere raw model of train.rs:100-126 (out: 7*7+4 floats). */
 void rmh_initial_model(float* raw_packed);
 
@@ -130,18 +142,33 @@ typedef struct rmh_collective {
   int (*all_reduce_sum)(void* state, float* buf, int64_t count, void* stream);
   int (*broadcast)(void* state, float* buf, int64_t count, int32_t root, void* stream);
   /* Nullable. Called by a rank that leaves rmh_train with an error after the collectives began:
-   * it must make the other ranks' pending and later collectives fail instead of waiting for this
-   * rank (the RCCL implementation aborts the communicator). */
+   * it releases this rank's side of the collectives (the RCCL implementation aborts its
+   * communicator, which ends its in-flight collectives). It does NOT reach the other ranks: a peer
+   * blocked in a collective with this rank leaves it through its own `wait` timeout, or is ended
+   * by the launcher (rm_train --ranks terminates the other ranks when one fails). */
   void (*abort)(void* state);
+  /* Nullable. The driver's only way of waiting for its stream while collectives may be in
+   * flight (instead of hipStreamSynchronize): returns RMH_OK once the stream drained, or an error
+   * when it did not within the implementation's timeout -- the RCCL one then aborts its
+   * communicator, so a rank whose peer died fails instead of spinning forever. */
+  int (*wait)(void* state, void* stream);
 } rmh_collective;
-/* RCCL communicator of rank `rank` of `world` on HIP device `device`. Rank 0 removes any file at
- * id_path, creates the ncclUniqueId and publishes it there (write + rename); the other ranks wait
- * up to timeout_s seconds for a file written after they started (an id file left by an earlier
- * run is never used); rank 0 removes the file once every rank has joined. id_path may be NULL
- * when world == 1. */
-int rmh_collective_rccl_create(int32_t rank, int32_t world, int32_t device, const char* id_path, double timeout_s,
-                               rmh_collective* out);
+/* RCCL communicator of rank `rank` of `world` on HIP device `device`. Rank 0 creates the
+ * ncclUniqueId and publishes it at id_path (rmh_rendezvous_publish); the other ranks wait up to
+ * timeout_s seconds for it (rmh_rendezvous_read) -- however late they start; rank 0 removes the
+ * file once every rank has joined. run_id (nullable: env RMH_RUN_ID, else TORCHELASTIC_RUN_ID,
+ * else "") tags the file, so a file left by an earlier run with another id is never used; with an
+ * empty id the launcher must give each run a fresh path or remove the file before starting the
+ * ranks. timeout_s is also the watchdog of `wait`. id_path may be NULL when world == 1. */
+int rmh_collective_rccl_create(int32_t rank, int32_t world, int32_t device, const char* id_path, const char* run_id,
+                               double timeout_s, rmh_collective* out);
 void rmh_collective_rccl_destroy(rmh_collective* c);
+/* The file rendezvous of rmh_collective_rccl_create, on any payload: publish writes
+ * [magic | run id | size | blob] to a temporary name and renames it to path (a stale file at path
+ * is removed first); read polls path until a complete file with the same run id and payload size
+ * appears (RMH_ERR_IO after timeout_s seconds, naming what the file there held). run_id as above. */
+int rmh_rendezvous_publish(const char* path, const char* run_id, const void* blob, int64_t size);
+int rmh_rendezvous_read(const char* path, const char* run_id, void* blob, int64_t size, double timeout_s);
 
 /* ---- train.rs: the driver ------------------------------------------------------------- */
 typedef struct rmh_train_config {
@@ -166,6 +193,19 @@ typedef struct rmh_train_config {
    * prune_and_split and broadcasts the next generation (its size, then its 7M'+4 raw params);
    * only rank 0 logs and writes files. Every rank ends with the same parameters. */
   const rmh_collective* comm;
+  /* Growth knobs of prune_and_split (rmh_prune_and_split_ex): 1, 0.05 and 0 (no cap), the
+   * reference rule. */
+  float split_scale;
+  float split_move;
+  int32_t max_spheres;
+  /* 1: fp16 colour / fp32 SDF (BASELINE configs[4], RM_MARCH_COLOR_F16): the renders read the
+   * activated colours as IEEE binary16, written by rm_optimizer_step_f16; parameters, moments and
+   * gradients stay fp32. 0: fp32 colours (the reference). */
+  int32_t color_f16;
+  /* Nullable. Called on every rank after each stage's training, before prune_and_split, with the
+   * stage's trained RAW packed parameters (host memory, valid during the call). */
+  void (*on_generation)(void* user, int32_t stage, int32_t num_spheres, const float* raw_packed);
+  void* user;
 } rmh_train_config;
 void rmh_train_config_default(rmh_train_config* cfg);
 

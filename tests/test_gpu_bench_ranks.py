@@ -32,6 +32,11 @@ def test_bench_two_ranks_gloo_rehearsal():
     assert d["config"]["parallelism"].startswith("views-dp2")
     assert d["value"] > 0 and d["finite"]
     assert abs(d["value"] - d["config"]["rays_per_step"] / (d["ms_per_step"] * 1e-3) / 1e6) <= 0.01 * d["value"]
+    # where a multi-rank step's time goes: per-rank train-kernel and all-reduce times
+    rk = d["ranks"]
+    assert len(rk["train_kernel_ms_per_step"]) == 2 and len(rk["allreduce_ms_per_step"]) == 2
+    assert 0 < rk["train_kernel_ms_min_max"][0] <= rk["train_kernel_ms_min_max"][1]
+    assert all(x >= 0 for x in rk["allreduce_ms_per_step"]) and rk["allreduce_bytes"] == 4 * (7 * 256 + 5)
 
 
 @pytest.mark.timeout(400)

@@ -292,3 +292,69 @@ def test_prune_everything_is_an_error(H):
     raw = _pack([[5.0, 0, 0]], [[0, 0, 0]], [-3.0])
     with pytest.raises(H.HostError, match="every sphere"):
         H.prune_and_split(raw, 1, [[5.0, 0, 0]], 0, 5, H.Rng(0))
+
+
+def test_split_knobs(H):
+    """rmh_prune_and_split_ex: (1, 0.05) is the reference rule bit for bit; (0, 0) splits every
+    surviving sphere; the pruning rules stay."""
+    stage, stages = 1, 5
+    r_raw = np.float32(np.log(np.expm1(np.float32(0.05))))  # softplus 0.05 < 0.25 * 0.65
+    c0 = np.float32([[0.0, 0.0, 0.0], [0.0, 0.0, 0.0], [1.3, 0.0, 0.0]])
+    c = np.float32([[0.2, 0.1, 0.0], [0.0, 0.0, 0.0], [1.3, 0.0, 0.0]])  # moved, not moved, pruned (far)
+    raw = _pack(c, np.ones((3, 3), np.float32), [r_raw, r_raw, r_raw])
+    ref, m_ref = H.prune_and_split(raw, 3, c0, stage, stages, H.Rng(7))
+    same, m_same = H.prune_and_split(raw, 3, c0, stage, stages, H.Rng(7), split_scale=1.0, split_move=0.05)
+    assert m_ref == m_same == 2 and np.array_equal(ref, same)  # nothing splits under the reference rule
+    out, m = H.prune_and_split(raw, 3, c0, stage, stages, H.Rng(7), split_scale=0.0, split_move=0.0)
+    assert m == 3  # sphere 0 split (moved), sphere 1 kept (move 0 is not > 0), sphere 2 pruned
+    out, m = H.prune_and_split(raw, 3, c0, stage, stages, H.Rng(7), split_scale=0.1, split_move=0.0)
+    assert m == 3  # 0.05 > 0.1 * 0.1625
+    _, m_last = H.prune_and_split(raw, 3, c0, stages - 1, stages, H.Rng(7), split_scale=0.0, split_move=0.0)
+    assert m_last == 2  # the last stage never splits
+    with pytest.raises(H.HostError):
+        H.prune_and_split(raw, 3, c0, stage, stages, H.Rng(7), split_scale=-1.0, split_move=0.0)
+    # the cap: six moved spheres that would all split; at most 9 in the next generation
+    c6 = np.float32([[0.1 * i, 0.05, 0.0] for i in range(6)])
+    raw6 = _pack(c6, np.ones((6, 3), np.float32), [r_raw] * 6)
+    z6 = np.zeros((6, 3), np.float32)
+    out, m = H.prune_and_split(raw6, 6, z6, stage, stages, H.Rng(7), split_scale=0.0, split_move=0.0)
+    assert m == 12
+    out, m = H.prune_and_split(raw6, 6, z6, stage, stages, H.Rng(7), split_scale=0.0, split_move=0.0, max_spheres=9)
+    assert m == 9  # the first three split (2 + 2 + 2 + 3 kept), in order
+    assert np.array_equal(out[18:27].reshape(3, 3), c6[3:])
+
+
+# ---- the RCCL id rendezvous (rmh_rendezvous_*, used by rmh_collective_rccl_create) -----------
+def test_rendezvous_late_reader(H, tmp_path):
+    """A rank that starts (or finishes its HIP init) long after rank 0 published the id still
+    takes it: no clock is involved (the former mtime check rejected it)."""
+    import threading
+    import time
+    path = str(tmp_path / "id")
+    blob = bytes(range(128))
+    H.rendezvous_publish(path, "run-A", blob)
+    time.sleep(2.5)
+    assert H.rendezvous_read(path, "run-A", len(blob), 5.0) == blob
+    # a reader that starts before the file exists waits for it
+    got = {}
+    t = threading.Thread(target=lambda: got.setdefault("b", H.rendezvous_read(path + "2", "run-B", 16, 10.0)))
+    t.start()
+    time.sleep(0.5)
+    H.rendezvous_publish(path + "2", "run-B", b"x" * 16)
+    t.join()
+    assert got["b"] == b"x" * 16
+
+
+def test_rendezvous_rejects_other_runs_file(H, tmp_path):
+    path = str(tmp_path / "id")
+    H.rendezvous_publish(path, "old-run", b"y" * 16)
+    with pytest.raises(H.HostError, match="run id 'old-run', expected 'new-run'"):
+        H.rendezvous_read(path, "new-run", 16, 0.3)
+    with pytest.raises(H.HostError, match="wrong payload size"):
+        H.rendezvous_read(path, "old-run", 8, 0.3)
+    # the environment supplies the run id when the argument is NULL
+    os.environ["RMH_RUN_ID"] = "old-run"
+    try:
+        assert H.rendezvous_read(path, None, 16, 1.0) == b"y" * 16
+    finally:
+        del os.environ["RMH_RUN_ID"]

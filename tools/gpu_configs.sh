@@ -7,6 +7,8 @@
 #   C4 1024x1024 / 1024 / 64 steps, 4 views (the per-GPU share of 32 views on 8 GPUs)
 #   C4s the same 32 views on one GPU (strong-scaling N = 1 leg)
 #   C5 512x512 / 4096 / 128 steps, 1 view (fp32 and fp16 colour)     k5: the metric at k = 5
+#   C2cj / C3cj: C2 / C3 on the data/cameras.json poses (C2 on the reference's own target PNGs)
+#   C5g: configs[4] on a model GROWN to 4096 spheres by prune_and_split (see grow below)
 #   bash tools/gpu_configs.sh <tag> [names...]   (CALIB=<fetch_calibration.json>: calibrated traffic)
 set -o pipefail
 export TMPDIR=/tmp
@@ -34,7 +36,28 @@ run() {
   fi
   python3 -c "import json,sys; d=json.load(open('$O/$name.json')); r=d['roofline']; print(sys.argv[1], d['value'], d['ms_per_step'], r['kernel_ms_per_step'], r['frac'], r['executed_frac'], (r['canonical'] or {}).get('frac'), d['finite'])" "$name" || return 1
 }
+# configs[4] as stated: a model grown to 4096 spheres through prune_and_split (rm_train: every
+# surviving sphere splits, capped at 4096; 11 stages x 100 steps at 512x512 / 128 steps / fp16
+# colours on the generate.rs targets rendered at 512x512 from the data/cameras.json poses)
+G=$O/grown
+grow() {
+  if [ -n "$ONLY" ] && [[ " $ONLY " != *" C5g "* ]]; then return 0; fi
+  mkdir -p $G/data
+  timeout -k 10 120 burn_raymarching_amd/lib/rm_train generate --out $G/data --prefix "" --size 512x512 > $G/generate.log 2>&1 && \
+  timeout -k 10 600 burn_raymarching_amd/lib/rm_train train --cameras $G/data/cameras.json --out $G --size 512x512 \
+    --march-steps 128 --color-f16 --stages 11 --steps 100 --split-scale 0 --split-move 0 --max-spheres 4096 \
+    --log-every 100 --no-previews > $G/train.log 2>&1 || { tail $G/train.log; return 1; }
+  GM=$(python3 -c "import json; print(len(json.load(open('$G/scene.json'))['radii']))")
+  grep -E "Stage|Next N|num_spheres" $G/train.log
+}
 run C2 256x256_M64_S32_V10 --width 256 --height 256 --spheres 64 --march-steps 32 --views-per-gpu 10 --steps 20 && \
+run C2cj 256x256_M64_S32_V10_cj --width 256 --height 256 --spheres 64 --march-steps 32 --views-per-gpu 10 --steps 20 \
+  --cameras tests/golden/cameras.json --targets files && \
+run C3cj 512x512_M256_S64_V10_cj --march-steps 64 --views-per-gpu 10 --steps 20 --cameras tests/golden/cameras.json \
+  --targets dango && \
+grow && \
+run C5g 512x512_M${GM}_S128_V1_c16_cj_grown --march-steps 128 --views-per-gpu 1 --steps 6 --warmup 2 --color-dtype f16 \
+  --cameras $G/data/cameras.json --targets files --scene-json $G/scene.json && \
 run C3 512x512_M256_S64_V10 --march-steps 64 --views-per-gpu 10 --steps 20 && \
 run C4 1024x1024_M1024_S64_V4 --width 1024 --height 1024 --spheres 1024 --march-steps 64 --views-per-gpu 4 --steps 6 --warmup 2 && \
 run C4s 1024x1024_M1024_S64_V32 --width 1024 --height 1024 --spheres 1024 --march-steps 64 --global-views 32 --steps 3 --warmup 1 && \
