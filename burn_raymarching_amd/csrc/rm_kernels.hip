@@ -2435,7 +2435,9 @@ __global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restric
   // the segments and scatters them (finalize_block, the bits of rm_finalize_grads). Hand-off
   // (MI355X_MICROARCH.md, inter-workgroup visibility): write-through segment stores drained by
   // every wave before the block barrier, one lane's agent-scope arrival, an agent-scope acquire
-  // and write-through-cache loads in the last block.
+  // and write-through-cache loads in the last block -- the guide's write-through variant of the
+  // counter hand-off, which needs no release fence (cdna_hip_programming.md §5 split-K item 2);
+  // stressed under uneven load against the two-launch reduction in tests/test_gpu_fusion.py.
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {

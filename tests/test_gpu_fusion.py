@@ -77,3 +77,32 @@ def test_small_optimizer_matches_two_kernel_path(mods, monkeypatch, m):
         res[flag] = (sm.raw.clone(), pen.clone(), sm.activated_packed().clone())
     for a, b in zip(res["1"], res["0"]):
         assert torch.allclose(a, b, rtol=1e-5, atol=1e-6), (a - b).abs().max()
+
+
+@pytest.mark.timeout(240)
+def test_reduce_handoff_stress_under_uneven_load(mods, monkeypatch):
+    """The in-launch hand-offs (rm_reduce_partials' last-arriving segment block, the small kernel's
+    last block): write-through (sc1) record stores drained by every storing wave before the block
+    barrier, one lane's relaxed agent-scope arrival, an agent-scope acquire in the last block
+    (MI355X_MICROARCH.md, inter-workgroup visibility: the write-through form that needs no release
+    fence). Stressed where stale data would show: many column blocks and segments (4096 spheres:
+    129 column blocks x 128 segments), repeated, while another stream keeps the CUs unevenly busy
+    and the consumers' L1 warm; every result bitwise equal to the two-launch reduction
+    (RM_REDUCE_FUSED=0), whose pass 2 reads after a kernel boundary."""
+    torch, model, _, render = mods
+    cases = ((4096, 2, 64), (1100, 1, 96), (24, 4, 64))  # the last: the small kernel's hand-off
+    monkeypatch.setenv("RM_REDUCE_FUSED", "0")
+    ref = {c: _train(torch, model, render, *c, 24) for c in cases}  # idle chip, two-launch reduction
+    monkeypatch.setenv("RM_REDUCE_FUSED", "1")
+    side = torch.cuda.Stream()
+    a = torch.randn(4096, 4096, device="cuda")
+    for it in range(6):
+        with torch.cuda.stream(side):  # uneven load: a GEMM stream competing for the CUs
+            for _ in range(1 + it % 3):
+                a = torch.tanh(a @ a * 1e-3)
+        for c in cases:
+            got = _train(torch, model, render, *c, 24)
+            assert torch.equal(got[0], ref[c][0]), (it, c)
+            for k in KEYS:
+                assert torch.equal(got[1][k], ref[c][1][k]), (it, c, k)
+    torch.cuda.synchronize()
