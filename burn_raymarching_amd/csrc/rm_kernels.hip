@@ -96,7 +96,8 @@ constexpr long long kSplitMaxRaysWide = 1048576;
 #define RM_SPLIT_WAVES 4
 #endif
 #ifndef RM_SPLIT_MIN_WAVES
-#define RM_SPLIT_MIN_WAVES 4  // register budget of the split kernels (waves per SIMD; 5: 168 VGPR spills)
+#define RM_SPLIT_MIN_WAVES 3  // register budget of the split kernels (waves per SIMD): 3 = 168 VGPRs, no
+                              // spills (4: 128 VGPRs, 4-12 VGPR spills, 20 B/lane scratch; C5 equal either way)
 #endif
 constexpr int kSplitWaves = RM_SPLIT_WAVES;  // waves per 64-ray block of the split march (2 or 4)
 static_assert(kSplitWaves == 2 || kSplitWaves == 4, "split blocks have 2 or 4 waves");

@@ -167,6 +167,17 @@ def test_fp32_gradient_error_within_gpu_bounds(oracle):
         g64 = oracle.render_diff_backward(o.astype(np.float64), d.astype(np.float64), sc, steps, k,
                                           g.astype(np.float64), precision="f64")
         within(oracle.render_diff_backward(o, d, sc, steps, k, g, precision="f32"), g64, "bwd")
+    # the split-march cases of tests/test_gpu_split.py::test_split_against_oracle (two 48x48 views)
+    cams = model.ring_cameras(10, offset=4)[:2]
+    rays = [oracle.camera_rays(48, 48, *c, precision="f32") for c in cams]
+    o = np.concatenate([r[0] for r in rays])
+    d = np.concatenate([r[1] for r in rays])
+    g = np.random.default_rng(3).normal(size=o.shape).astype(np.float32)
+    for m in (256, 300, 1100):
+        sc = model.synthetic_scene(m, 11, radius_range=(0.02, 0.08))
+        g64 = oracle.render_diff_backward(o.astype(np.float64), d.astype(np.float64), sc, 32, 32.0,
+                                          g.astype(np.float64), precision="f64")
+        within(oracle.render_diff_backward(o, d, sc, 32, 32.0, g, precision="f32"), g64, "bwd")
     sc = model.synthetic_scene(256, 2)
     o, d = oracle.camera_rays(64, 64, *model.ring_cameras(10, offset=3)[0], precision="f32")
     o64, d64 = o.astype(np.float64), d.astype(np.float64)
