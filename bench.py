@@ -540,6 +540,12 @@ def main():
     if traffic is None:
         traffic, traffic_src = _latest_profile("r*_pmc_traffic.json", key, "train_kernel_bytes_per_launch")
         traffic_basis = "per launch"
+    # the same profile's uncalibrated sum and calibration, so that the line states which figure it quotes
+    tdetail, _ = _latest_profile(os.path.basename(traffic_src) if traffic_src else "none", key, "detail")
+    traffic_raw = None
+    if tdetail and tdetail.get("raw_bytes_per_launch") is not None:
+        per_step = tdetail["launches"] / max(tdetail.get("steps") or tdetail["launches"], 1)
+        traffic_raw = tdetail["raw_bytes_per_launch"] * (per_step if traffic_basis == "per step" else 1.0)
     pmc, pmc_src = _latest_profile("r*_pmc_sq.json", key, "train_kernel")
     alg_bytes = rays_per_rank * BYTES_PER_RAY_CAMERA  # per step (all of this rank's rays)
     mpad = (M + 31) // 32 * 32
@@ -567,6 +573,11 @@ def main():
         "traffic": traffic,
         "traffic_source": traffic_src,
         "traffic_basis": traffic_basis,
+        "traffic_kind": None if traffic is None else (
+            "FETCH_SIZE x read factor + WRITE_SIZE x write factor, factors measured on known byte counts "
+            "(tools/fetch_calib)" if tdetail and tdetail.get("calibration") else "raw FETCH_SIZE + WRITE_SIZE"),
+        "traffic_raw": None if traffic_raw is None else round(traffic_raw),
+        "traffic_calibration": None if not tdetail else tdetail.get("calibration"),
         "kernel_ms": round(kern_avg_ms, 4),
         "kernel_ms_per_step": round(kern_step_ms, 4),
         "launches_timed": launches,
