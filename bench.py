@@ -116,6 +116,10 @@ def parse():
                     help="start from this scene.json (train.rs:238-262 layout, radius + 0.01 re-added as scene.rs:43) "
                          "instead of the synthetic seed-0 scene; --spheres is taken from the file (e.g. a model grown "
                          "by `rm_train train --split-scale 0 --split-move 0`, BASELINE configs[4])")
+    ap.add_argument("--graph", choices=["on", "off"], default="off",
+                    help="on (one GPU): capture one training step in a hipGraph (torch.cuda.CUDAGraph over the rm_* "
+                         "calls, per-step scalars on the device: rm_bind_step_scalars) and replay it for the timed "
+                         "steps; the train-kernel time then comes from the statistics replay (eager, timed)")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--kernel-timing", choices=["on", "off"], default="on",
@@ -257,6 +261,11 @@ def main():
             raise SystemExit("bench.py needs a HIP device")
         local %= torch.cuda.device_count()
     torch.cuda.set_device(local)
+    use_graph = args.graph == "on"
+    if use_graph:
+        if world > 1:
+            raise SystemExit("--graph on is for one GPU (the N-rank step keeps its all-reduce eager)")
+        torch.cuda.set_stream(torch.cuda.Stream())  # a capturable stream for every call of the run
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -379,6 +388,13 @@ def main():
             loss_out.copy_(tot[nm:])
 
     dp = ViewShardedStep(shard, npix, rmm.packed_size(M), "cuda", step_fn, optim_fn=lambda g: opt.step(g, args.lr))
+    # graph mode: progress and Adam's step from a device record the optimizer advances (the
+    # eager steps of the run read it too, so eager and replayed steps compute the same thing)
+    sdev = None
+    if use_graph:
+        sdev = torch.tensor([1, 0, total_steps, 0], dtype=torch.int32, device="cuda")
+        for cx in ctxs:
+            cx.bind_step_scalars(sdev.data_ptr())
     loss = dp.loss
     grad0 = []
 
@@ -392,7 +408,7 @@ def main():
         step(i)
     # snapshot of the training state at the start of the timed region (for the untimed replays)
     snap = (model.raw.clone(), model._act.clone(), opt.m.clone(), opt.v.clone(), opt.t,
-            None if model._col_h is None else model._col_h.clone())
+            None if model._col_h is None else model._col_h.clone(), None if sdev is None else sdev.clone())
 
     def restore():
         model.raw.copy_(snap[0])
@@ -402,7 +418,17 @@ def main():
         opt.t = snap[4]
         if snap[5] is not None:
             model._col_h.copy_(snap[5])
+        if snap[6] is not None:
+            sdev.copy_(snap[6])
         model._act_valid = True
+
+    graph = None
+    if use_graph:  # one step captured (not run: the record is not advanced), replayed per timed step
+        torch.cuda.synchronize()
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph, stream=torch.cuda.current_stream()):
+            step(args.warmup)
+        torch.cuda.synchronize()
 
     torch.cuda.synchronize()
     ctx.collect_timing(reset=True)
@@ -418,13 +444,16 @@ def main():
     t0 = time.perf_counter()
     timed_steps = 0
     for j, i in enumerate(range(args.warmup, total_steps)):
-        timed = args.kernel_timing == "on" and j % every == 0
+        timed = args.kernel_timing == "on" and j % every == 0 and graph is None
         ctx.timing(timed)
         dp.time_allreduce = timed
         timed_steps += timed
         if ev[j] is not None:
             ev[j][0].record()
-        step(i)
+        if graph is None:
+            step(i)
+        else:
+            graph.replay()
         if ev[j] is not None:
             ev[j][1].record()
     host_s = time.perf_counter() - t0  # host time to submit the K steps (before the final sync)
@@ -454,7 +483,15 @@ def main():
     if args.aux_steps > 0:
         ctx.stats(True)
         ctx.collect_stats(reset=True)
-        replay(lambda j: None)
+        if graph is not None and args.kernel_timing == "on":
+            # graph mode: the train kernel timed on this eager replay of the same steps
+            ctx.collect_timing(reset=True)
+            replay(lambda j: ctx.timing(j % every == 0))
+            ctx.timing(False)
+            kern_ms, launches = ctx.collect_timing(reset=True)
+            timed_steps = sum(1 for j in range(args.steps) if j % every == 0)
+        else:
+            replay(lambda j: None)
         st = ctx.collect_stats(reset=True)
         ctx.stats(False)
         if args.kernel_timing == "on":  # the same steps with the early exit off (full work per ray)
@@ -624,7 +661,7 @@ def main():
                                    + (", fp16 colour / fp32 SDF" if args.color_dtype == "f16" else ""),
                        "width": W, "height": H, "spheres": M, "march_steps": S, "smooth_k": K,
                        "views_per_gpu": vpg, "global_views": shard.views_total, "views_per_call": views_per_call,
-                       "streams": nstreams,
+                       "streams": nstreams, "graph": use_graph,
                        "ring": ring, "ring_order": args.ring_order, "rays_per_step": rays_global, "radius_range": list(rr),
                        "color_storage": args.color_dtype, "sdf_dtype": "f32",
                        "cameras": args.cameras and os.path.relpath(os.path.abspath(args.cameras), ROOT),

@@ -135,6 +135,11 @@ struct KArgs {
   int* olist_w;
   int* ocnt_w;
   int* ocnt_z;
+  // nullable: the device word naming the list set this launch appends to (0..2); with it the five
+  // pointers above point to set 0 and the launch picks its sets from the word (read: the set
+  // before, clear: the set after), and the call's reduction advances the word -- the rotation
+  // lives on the device, so a launch captured in a hipGraph keeps rotating when replayed
+  const int* oturn;
   CamBasis cams[kInlineCams];  // views <= kInlineCams
   const CamBasis* cams_dev;    // more views: the bases in device memory (cams unused), else NULL
   // activated scene
@@ -157,6 +162,7 @@ struct KArgs {
   const float* gout;
   const float* targets;
   float progress, inv_count;
+  const rm_step_scalars* sdev;  // nullable (rm_bind_step_scalars): progress = index / total from here
   float light_fixed[3];  // kRender: renderer.rs:27-32 light, normalised on the host in f32
   float* dbg;       // optional per-ray intermediates [n][16] (diagnostics; see rm_debug_intermediates)
   float* partials;  // [gridDim.x][rec], rec = Mpad*8 + 8
@@ -1123,6 +1129,34 @@ __device__ __forceinline__ bool escapes(const float o[3], const float d[3], floa
   return tau >= tc && g(tau) >= (double)min_d;
 }
 
+// The cost-ordered dispatch's list sets of this launch: with a.oturn the pointers of KArgs are
+// set 0's and the sets follow the device turn word w: read (w + 2) % 3, append w, clear (w + 1) % 3.
+struct OrderSets {
+  const int* list_r;
+  const int* cnt_r;
+  int* list_w;
+  int* cnt_w;
+  int* cnt_z;
+};
+__device__ __forceinline__ OrderSets order_sets(const KArgs& a) {
+  OrderSets o{a.olist_r, a.ocnt_r, a.olist_w, a.ocnt_w, a.ocnt_z};
+  if (a.oturn != nullptr) {
+    const int w = __builtin_amdgcn_readfirstlane(*a.oturn);
+    const int r = (w + 2) % 3, z = (w + 1) % 3;
+    constexpr long long kSet = (long long)RM_ORDER_CLASSES * kMaxBlocksPerLaunch;
+    if (o.list_r != nullptr) {
+      o.list_r += r * kSet;
+      o.cnt_r += r * RM_ORDER_CLASSES;
+    }
+    if (o.list_w != nullptr) {
+      o.list_w += w * kSet;
+      o.cnt_w += w * RM_ORDER_CLASSES;
+    }
+    if (o.cnt_z != nullptr) o.cnt_z += z * RM_ORDER_CLASSES;
+  }
+  return o;
+}
+
 // Launch position -> logical ray block. With block_order (whole 16x16-tiled views per launch) the
 // blocks are dispatched tile rank by tile rank, the views interleaved, in the order of
 // block_order: the tiles nearest the image centre -- where the scene usually is, and so the
@@ -1144,13 +1178,14 @@ __device__ __forceinline__ long long ray_block(const KArgs& a, int* cls = nullpt
   const int g = b >> 3;
   if ((g + 1) * 8 <= (int)gridDim.x) b = (g << 3) + (((b & 7) + g) & 7);
 #endif
-  if (a.ocnt_r != nullptr) {
+  const OrderSets os = order_sets(a);
+  if (os.cnt_r != nullptr) {
     // position b of the class-major concatenation of the previous launch's lists; every block
     // reads the same counts, so a short total (never expected) sends all blocks to the static order
     int tot = 0, cb = -1, base = 0;
 #pragma unroll
     for (int c = 0; c < RM_ORDER_CLASSES; ++c) {
-      const int n = a.ocnt_r[c];
+      const int n = os.cnt_r[c];
       if (cb < 0 && b < tot + n) {
         cb = c;
         base = tot;
@@ -1159,7 +1194,7 @@ __device__ __forceinline__ long long ray_block(const KArgs& a, int* cls = nullpt
     }
     if (tot == (int)gridDim.x && cb >= 0) {
       if (cls != nullptr) *cls = cb;
-      return a.olist_r[cb * kMaxBlocksPerLaunch + (b - base)];
+      return os.list_r[cb * kMaxBlocksPerLaunch + (b - base)];
     }
   }
   const int r = b / a.order_views, v = b - r * a.order_views;
@@ -1172,10 +1207,18 @@ __device__ __forceinline__ void order_append(const KArgs& a, long long blk, int 
   constexpr int kCls = RM_ORDER_CLASSES;
   const float cls_scale = (float)kCls / (float)((a.split ? 1 : kWaves) * (a.steps + kPostCost) + 1);
   const int c = kCls - 1 - (int)fminf((float)cost * cls_scale, (float)(kCls - 1));
-  const int idx = atomicAdd(a.ocnt_w + c, 1);
+  const OrderSets os = order_sets(a);
+  const int idx = atomicAdd(os.cnt_w + c, 1);
   // counts left uncleared (a failed launch in the rotation) overrun the total, and ray_block
   // then falls back to the static order: never write past the list
-  if (idx < kMaxBlocksPerLaunch) a.olist_w[c * kMaxBlocksPerLaunch + idx] = (int)blk;
+  if (idx < kMaxBlocksPerLaunch) os.list_w[c * kMaxBlocksPerLaunch + idx] = (int)blk;
+}
+
+// compute_loss's progress (training.rs:17-34 weights): the call's argument, or with device step
+// scalars bound (rm_bind_step_scalars) index / total in fp32 as train.rs:171-172 forms it.
+__device__ __forceinline__ float progress_of(const KArgs& a) {
+  if (a.sdev == nullptr) return a.progress;
+  return fminf((float)a.sdev->index / (float)a.sdev->total, 1.0f);
 }
 
 // A block of escaping rays: out = 0 (requested outputs), zero gradient partials, and for the
@@ -1193,7 +1236,7 @@ __device__ __forceinline__ void escaped_block(const KArgs& a, const Lds& L, long
   float loss = 0.0f;
   if (MODE == kTrain && valid) {  // training.rs:17-34 with out = 0
     const float t0 = a.targets[3 * ri], t1 = a.targets[3 * ri + 1], t2 = a.targets[3 * ri + 2];
-    const float W = (t0 + t1 + t2) > 0.01f ? 10.0f : fmaf(a.progress, 4.0f, 1.0f);
+    const float W = (t0 + t1 + t2) > 0.01f ? 10.0f : fmaf(progress_of(a), 4.0f, 1.0f);
     const float tg[3] = {t0, t1, t2};
 #pragma unroll
     for (int c = 0; c < 3; ++c) loss = fmaf(fabsf(0.0f - tg[c]), W, loss);
@@ -1360,7 +1403,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   // ---- escape skip (RM_MARCH_SKIP_ESCAPED): a block whose rays all provably leave the scene
   // (rm_escape_kernel) gets out = 0 and zero gradients without marching -- exactly what the full
   // computation yields for them, since their silhouette mask is 0 in f32 (see escapes()).
-  if (a.ocnt_z != nullptr && blockIdx.x == 0 && tid < RM_ORDER_CLASSES) a.ocnt_z[tid] = 0;
+  if (a.ocnt_z != nullptr && blockIdx.x == 0 && tid < RM_ORDER_CLASSES) order_sets(a).cnt_z[tid] = 0;
   if (a.esc_flags != nullptr && a.esc_flags[blk]) {
     if (a.stats != nullptr && tid == 0) atomicAdd(a.stats, 1ull);
     if (a.ocnt_w != nullptr && tid == 0) order_append(a, blk, 0);
@@ -1923,7 +1966,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       g[2] = a.gout[3 * ri + 2];
     } else {  // training.rs:17-34
       const float t0 = a.targets[3 * ri], t1 = a.targets[3 * ri + 1], t2 = a.targets[3 * ri + 2];
-      const float W = (t0 + t1 + t2) > 0.01f ? 10.0f : fmaf(a.progress, 4.0f, 1.0f);
+      const float W = (t0 + t1 + t2) > 0.01f ? 10.0f : fmaf(progress_of(a), 4.0f, 1.0f);
       const float tg[3] = {t0, t1, t2};
 #pragma unroll
       for (int c = 0; c < 3; ++c) {
@@ -2372,6 +2415,7 @@ struct FinalArgs {
   const float* light_dir;
   float *gc, *gcol, *gr, *gld, *gamb, *loss_sum;
   int accumulate;
+  int* oturn;  // nullable: the cost-order turn word the reduction advances (KArgs::oturn)
 };
 
 #ifndef RM_REDUCE_BATCH
@@ -2401,6 +2445,8 @@ __global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restric
   __shared__ int last;
   const int ncols = Mpad * 8 + 8;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the launch whose partials these are has finished: the cost-ordered dispatch turns one set on
+  if (f.oturn != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *f.oturn = (*f.oturn + 1) % 3;
   const int col = blockIdx.x * 256 + tid;
   const bool scalars = (int)blockIdx.x * 256 >= Mpad * 8;  // the column block of the 8 scalars
   const int b0 = blockIdx.y * seg_len;
@@ -2820,8 +2866,10 @@ __global__ __launch_bounds__(256) void rm_optimizer_kernel(const float* __restri
                                                            float lr, float wd, int with_pen,
                                                            float* __restrict__ pen_parts,
                                                            float* __restrict__ act_out,
-                                                           _Float16* __restrict__ col_h_out) {
+                                                           _Float16* __restrict__ col_h_out,
+                                                           const rm_step_scalars* __restrict__ sdev) {
   __shared__ float red[4 * 256];
+  if (sdev != nullptr) step = sdev->step;  // device step scalars (rm_bind_step_scalars)
   const int i = blockIdx.x * 256 + threadIdx.x;
   const int n = 7 * M + 4;
   float pen = 0.0f;
@@ -2930,12 +2978,29 @@ __global__ __launch_bounds__(256) void rm_optimizer_small(float* __restrict__ ra
                                                           float* __restrict__ m1, float* __restrict__ m2, int M,
                                                           int step, float lr, float wd, int with_pen,
                                                           float* __restrict__ loss_penalty, float* __restrict__ act_out,
-                                                          _Float16* __restrict__ col_h_out) {
+                                                          _Float16* __restrict__ col_h_out,
+                                                          rm_step_scalars* __restrict__ sdev) {
   const OptPrefetch pf = opt_prefetch(raw, m1, m2, M);
+  if (sdev != nullptr) step = sdev->step;  // device step scalars (rm_bind_step_scalars)
   const int n = 7 * M + 4, i0 = (int)threadIdx.x;
   const float g[2] = {i0 < n ? gact[i0] : 0.0f, i0 + 256 < n ? gact[i0 + 256] : 0.0f};
   const OptPre o = opt_small_pre(pf, M, step, with_pen, loss_penalty);
   opt_small_post(o, pf, g, raw, m1, m2, M, lr, wd, act_out, col_h_out);
+  if (sdev != nullptr) {  // every thread has read the step: the training step ends here
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      sdev->step += 1;
+      sdev->index += 1;
+    }
+  }
+}
+
+// The end of a training step with device step scalars bound (multi-block optimizer path).
+__global__ void rm_step_advance(rm_step_scalars* sdev) {
+  if (threadIdx.x == 0) {
+    sdev->step += 1;
+    sdev->index += 1;
+  }
 }
 
 __global__ void rm_sum_small(const float* __restrict__ parts, int n, float* __restrict__ out) {
@@ -2956,6 +3021,7 @@ __global__ void rm_sum_small(const float* __restrict__ parts, int n, float* __re
 struct rm_context {
   int device = 0;
   hipStream_t stream = nullptr;
+  rm_step_scalars* sdev = nullptr;  // device step scalars (rm_bind_step_scalars), nullable
   std::string err;
   void* ws = nullptr;  // partials | segment sums | small scratch
   size_t ws_bytes = 0;
@@ -2983,7 +3049,7 @@ struct rm_context {
   int* ocnt = nullptr;                      // 3 x [class] list lengths (zeroed one launch ahead)
   float* cont_buf = nullptr;                // split continuation: saved march state | list | count
   size_t cont_bytes = 0;
-  int oturn = 0;                            // the list set the next keyed launch appends to
+  int* oturn = nullptr;                     // device word: the list set the next keyed launch appends to
   unsigned long long cost_key = 0;          // geometry of the last keyed launch (its lists order the next)
   bool cost_valid = false;
 #ifdef RM_BLOCK_TRACE
@@ -3197,12 +3263,15 @@ FinalArgs final_args(const Call& c, bool first) {
   fa.gamb = gp->ambient;
   fa.loss_sum = c.mode == kTrain ? c.loss_sum : nullptr;
   fa.accumulate = first ? c.accumulate : 1;
+  fa.oturn = nullptr;
   return fa;
 }
 
 // The fixed-order cross-block reduction of a launch's nb partial records (a.partials) and the
 // gradient scatter into the caller's layout (rm_reduce_partials + rm_finalize_grads).
 int reduce_and_finalize(rm_context* ctx, const Call& c, const KArgs& a, long long nb, bool first) {
+  FinalArgs fa = final_args(c, first);
+  fa.oturn = const_cast<int*>(a.oturn);  // a keyed launch: its reduction advances the turn
   const int nblocks = (int)nb;
   const int ncols = a.Mpad * 8 + 8;
   float* S = a.partials + (long long)std::max<long long>(nb, 1) * a.rec;
@@ -3219,7 +3288,7 @@ int reduce_and_finalize(rm_context* ctx, const Call& c, const KArgs& a, long lon
     RM_HIP(ctx, hipMemsetAsync(ctx->red_arrivals, 0, sizeof(unsigned) * kRedArrivals, ctx->stream));
   }
   hipLaunchKernelGGL(rm_reduce_partials, dim3((unsigned)xblocks, (unsigned)segs), dim3(256), 0, ctx->stream, a.partials,
-                     a.rec, a.M, a.Mpad, nblocks, seg_len, S, final_args(c, first), fused ? ctx->red_arrivals : nullptr);
+                     a.rec, a.M, a.Mpad, nblocks, seg_len, S, fa, fused ? ctx->red_arrivals : nullptr);
   RM_HIP(ctx, hipGetLastError());
   if (!fused) {
     hipLaunchKernelGGL(rm_finalize_grads, dim3((unsigned)((ncols + 63) / 64)), dim3(256), 0, ctx->stream, S, segs, a.M,
@@ -3466,6 +3535,7 @@ int run(rm_context* ctx, const Call& c) {
   a.targets = c.targets;
   a.progress = c.progress;
   a.inv_count = c.inv_count;
+  a.sdev = ctx->sdev;
   a.dbg = c.dbg;
   // Escape skipping needs the mask to be exactly 0 at the certified distance: sigmoid(-msharp D)
   // once msharp log2(e) D > 128 overflows exp2 (use 160), exp(-10 D^2) in kRender long before 50.
@@ -3576,6 +3646,7 @@ int run(rm_context* ctx, const Call& c) {
     a.olist_w = nullptr;
     a.ocnt_w = nullptr;
     a.ocnt_z = nullptr;
+    a.oturn = nullptr;
     const long long npix = (long long)c.W * c.H;
     if (c.cam && a.tiling == 2 && nb > 1 && done % npix == 0 && nr % npix == 0 && nr == nb * rpb &&
         (c.march->flags & RM_MARCH_NATURAL_ORDER) == 0) {
@@ -3594,23 +3665,23 @@ int run(rm_context* ctx, const Call& c) {
       constexpr int kCls = RM_ORDER_CLASSES;
       if (!ctx->olist) {
         RM_HIP(ctx, hipMalloc(&ctx->olist, sizeof(int) * 3 * kCls * kMaxBlocksPerLaunch));
-        RM_HIP(ctx, hipMalloc(&ctx->ocnt, sizeof(int) * 3 * kCls));
-        RM_HIP(ctx, hipMemsetAsync(ctx->ocnt, 0, sizeof(int) * 3 * kCls, ctx->stream));
-        ctx->oturn = 0;
+        RM_HIP(ctx, hipMalloc(&ctx->ocnt, sizeof(int) * (3 * kCls + 1)));  // + the turn word
+        RM_HIP(ctx, hipMemsetAsync(ctx->ocnt, 0, sizeof(int) * (3 * kCls + 1), ctx->stream));
+        ctx->oturn = ctx->ocnt + 3 * kCls;
       }
       // three list sets in rotation: the previous launch's (read), this launch's (appended;
-      // cleared by the previous launch) and the next launch's (cleared by this one)
-      const int wi = ctx->oturn, ri = (wi + 2) % 3, zi = (wi + 1) % 3;
+      // cleared by the previous launch) and the next launch's (cleared by this one); which is which
+      // the kernel reads from the device turn word, advanced by this call's reduction (order_sets)
       if (ctx->cost_valid && ctx->cost_key == key) {
-        a.olist_r = ctx->olist + (size_t)ri * kCls * kMaxBlocksPerLaunch;
-        a.ocnt_r = ctx->ocnt + ri * kCls;
+        a.olist_r = ctx->olist;
+        a.ocnt_r = ctx->ocnt;
       }
-      a.olist_w = ctx->olist + (size_t)wi * kCls * kMaxBlocksPerLaunch;
-      a.ocnt_w = ctx->ocnt + wi * kCls;
-      a.ocnt_z = ctx->ocnt + zi * kCls;
+      a.olist_w = ctx->olist;
+      a.ocnt_w = ctx->ocnt;
+      a.ocnt_z = ctx->ocnt;
+      a.oturn = ctx->oturn;
       if (const char* e = std::getenv("RM_DEBUG_SKIP_ORDER_CLEAR"))  // recovery test (rm_debug_order_counts)
         if (e[0] == '1') a.ocnt_z = nullptr;
-      ctx->oturn = zi;
     }
     if (has_rec) {
       ctx->cost_valid = key != 0;
@@ -3720,6 +3791,12 @@ int rm_create(int32_t device, void* stream, rm_context** out_ctx) {
   return RM_OK;
 }
 
+int rm_bind_step_scalars(rm_context* ctx, rm_step_scalars* dev) {
+  if (!ctx) return RM_ERR_INVALID_ARG;
+  ctx->sdev = dev;
+  return RM_OK;
+}
+
 int rm_set_stream(rm_context* ctx, void* stream) {
   if (!ctx) return RM_ERR_INVALID_ARG;
   ctx->stream = static_cast<hipStream_t>(stream);
@@ -3758,15 +3835,13 @@ int rm_debug_order_counts(rm_context* ctx, int32_t* counts, int32_t capacity, in
   if (!ctx) return RM_ERR_INVALID_ARG;
   constexpr int kCls = RM_ORDER_CLASSES;
   if (classes) *classes = kCls;
-  if (next_set) *next_set = ctx->oturn;
-  if (!counts) return RM_OK;
-  if (capacity < 3 * kCls) return fail(ctx, RM_ERR_INVALID_ARG, "counts needs %d entries", 3 * kCls);
+  if (counts && capacity < 3 * kCls) return fail(ctx, RM_ERR_INVALID_ARG, "counts needs %d entries", 3 * kCls);
   RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  if (!ctx->ocnt) {
-    for (int i = 0; i < 3 * kCls; ++i) counts[i] = 0;
-    return RM_OK;
-  }
-  RM_HIP(ctx, hipMemcpy(counts, ctx->ocnt, sizeof(int) * 3 * kCls, hipMemcpyDeviceToHost));
+  std::vector<int> host(3 * kCls + 1, 0);  // the counts and the device turn word
+  if (ctx->ocnt) RM_HIP(ctx, hipMemcpy(host.data(), ctx->ocnt, sizeof(int) * host.size(), hipMemcpyDeviceToHost));
+  if (next_set) *next_set = host[3 * kCls];
+  if (counts)
+    for (int i = 0; i < 3 * kCls; ++i) counts[i] = host[i];
   return RM_OK;
 }
 
@@ -4130,14 +4205,14 @@ int rm_optimizer_step_f16(rm_context* ctx, float* raw_packed, const float* grad_
   if (!raw_packed || !grad_act_packed || !adam_m || !adam_v)
     return fail(ctx, RM_ERR_INVALID_ARG, "NULL optimizer buffer");
   if (num_spheres < 1 || num_spheres > RM_MAX_SPHERES) return fail(ctx, RM_ERR_INVALID_ARG, "bad num_spheres");
-  if (step < 1) return fail(ctx, RM_ERR_INVALID_ARG, "step counts from 1");
+  if (step < 1 && !ctx->sdev) return fail(ctx, RM_ERR_INVALID_ARG, "step counts from 1");
   const int M = num_spheres;
   const int n = 7 * M + 4;
   const int nb = (n + 255) / 256;
   if (M <= rm::kOptSmallMaxM && !env_is("RM_OPT_SMALL", '0')) {  // one block: snapshot, repulsion rows, update
     hipLaunchKernelGGL(rm::rm_optimizer_small, dim3(1), dim3(256), 0, ctx->stream, raw_packed, grad_act_packed, adam_m,
                        adam_v, M, step, lr, weight_decay, with_penalties ? 1 : 0, loss_penalty, act_out,
-                       reinterpret_cast<_Float16*>(colors_f16_out));
+                       reinterpret_cast<_Float16*>(colors_f16_out), ctx->sdev);
     RM_HIP(ctx, hipGetLastError());
     return RM_OK;
   }
@@ -4153,8 +4228,12 @@ int rm_optimizer_step_f16(rm_context* ctx, float* raw_packed, const float* grad_
   RM_HIP(ctx, hipGetLastError());
   hipLaunchKernelGGL(rm::rm_optimizer_kernel, dim3(nb), dim3(256), 0, ctx->stream, snap, raw_packed,
                      grad_act_packed, adam_m, adam_v, pair, M, step, lr, weight_decay, with_penalties ? 1 : 0, parts,
-                     act_out, reinterpret_cast<_Float16*>(colors_f16_out));
+                     act_out, reinterpret_cast<_Float16*>(colors_f16_out), ctx->sdev);
   RM_HIP(ctx, hipGetLastError());
+  if (ctx->sdev) {
+    hipLaunchKernelGGL(rm::rm_step_advance, dim3(1), dim3(64), 0, ctx->stream, ctx->sdev);
+    RM_HIP(ctx, hipGetLastError());
+  }
   if (loss_penalty) {
     hipLaunchKernelGGL(rm::rm_sum_small, dim3(1), dim3(64), 0, ctx->stream, parts, nb, loss_penalty);
     RM_HIP(ctx, hipGetLastError());
@@ -4185,7 +4264,7 @@ int rm_train_iteration(rm_context* ctx, const float* ray_org, const float* ray_d
   if (num_src < 1 || num_src > INT32_MAX || n_uniform < 0 || n_fg < 0 || num_fg < 0)
     return fail(ctx, RM_ERR_INVALID_ARG, "bad sampling sizes");
   if (n_fg > 0 && (num_fg == 0 || !fg_indices)) return fail(ctx, RM_ERR_INVALID_ARG, "n_fg > 0 needs foreground indices");
-  if (step < 1) return fail(ctx, RM_ERR_INVALID_ARG, "step counts from 1");
+  if (step < 1 && !ctx->sdev) return fail(ctx, RM_ERR_INVALID_ARG, "step counts from 1");
   const int M = num_spheres;
   const long long n = n_uniform + n_fg;
   rm_scene sc;
@@ -4211,7 +4290,7 @@ int rm_train_iteration(rm_context* ctx, const float* ray_org, const float* ray_d
   const bool fused = use_small(c, M, n) && (n + rpb - 1) / rpb <= kSmallFinalMaxBlocks &&
                      (n + rpb - 1) / rpb <= max_blocks_per_launch() &&
                      M <= kOptSmallMaxM && !env_is("RM_SMALL_FINAL", '0') &&
-                     !env_is("RM_FUSED_ITER", '0');
+                     !env_is("RM_FUSED_ITER", '0') && ctx->sdev == nullptr;
   if (fused) {
     SmallArgs fz;
     std::memset(&fz, 0, sizeof fz);

@@ -541,7 +541,7 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
       g[2] = a.gout[3 * ri + 2];
     } else {
       const float t0 = tgv[0], t1 = tgv[1], t2 = tgv[2];
-      const float W = (t0 + t1 + t2) > 0.01f ? 10.0f : fmaf(a.progress, 4.0f, 1.0f);
+      const float W = (t0 + t1 + t2) > 0.01f ? 10.0f : fmaf(progress_of(a), 4.0f, 1.0f);
       const float tg[3] = {t0, t1, t2};
 #pragma unroll
       for (int c = 0; c < 3; ++c) {

@@ -64,6 +64,7 @@ SIGNATURES = {
     "rm_version": (ctypes.c_char_p, []),
     "rm_create": (ctypes.c_int, [_I32, _P, ctypes.POINTER(_P)]),
     "rm_set_stream": (ctypes.c_int, [_P, _P]),
+    "rm_bind_step_scalars": (ctypes.c_int, [_P, _P]),
     "rm_destroy": (None, [_P]),
     "rm_last_error": (ctypes.c_char_p, [_P]),
     "rm_march_default": (None, [ctypes.POINTER(RmMarch)]),
@@ -149,6 +150,12 @@ class Context:
     def _torch_stream(device):
         import torch
         return torch.cuda.current_stream(device).cuda_stream
+
+    def bind_step_scalars(self, dev_ptr):
+        """rm_bind_step_scalars: progress / Adam step of this context's calls from the device
+        record at dev_ptr ([step, index, total, reserved] int32; None unbinds)."""
+        self.check(self._lib.rm_bind_step_scalars(self.handle, _P(dev_ptr) if dev_ptr else None),
+                   "rm_bind_step_scalars")
 
     def set_stream(self, stream: int):
         self.check(self._lib.rm_set_stream(self.handle, _P(stream)), "rm_set_stream")

@@ -237,6 +237,28 @@ int rm_sample_batch(rm_context* ctx, const float* ray_org, const float* ray_dir,
                     uint64_t stream, uint64_t counter, float* out_org, float* out_dir, float* out_targets,
                     int32_t* indices_out);
 
+/* ---- hipGraph capture of a training step ----------------------------------- */
+/* A step's calls (train step, optimizer) can be captured once in a hipGraph
+ * (hipStreamBeginCapture on the context's stream ... hipStreamEndCapture, hipGraphInstantiate)
+ * and replayed with hipGraphLaunch. What changes from one step to the next lives on the device:
+ *  - the per-step scalars: while an rm_step_scalars record is bound to the context
+ *    (rm_bind_step_scalars), rm_train_step[_camera] take progress = min(index / total, 1) in fp32
+ *    (train.rs:171-172) instead of their `progress` argument, and rm_optimizer_step[_f16] take
+ *    Adam's step from `step` instead of their argument and then advance the record on the device
+ *    (step += 1, index += 1) -- the optimizer ends a training step;
+ *  - the cost-ordered dispatch rotates its list sets on the device by itself.
+ * rm_reserve before the capture keeps every call allocation-free; kernel timing (rm_timing_enable)
+ * and rm_train_iteration's one-launch form are not for capture (with a bound record,
+ * rm_train_iteration runs its three calls). dev = NULL unbinds; the record is the caller's device
+ * memory and must outlive the binding. */
+typedef struct rm_step_scalars {
+  int32_t step;     /* Adam's step of the next optimizer call (counts from 1) */
+  int32_t index;    /* the global step of the next train call ... */
+  int32_t total;    /* ... out of total: progress = index / total */
+  int32_t reserved;
+} rm_step_scalars;
+int rm_bind_step_scalars(rm_context* ctx, rm_step_scalars* dev);
+
 /* ---- diagnostics ------------------------------------------------------------ */
 /* Per-ray forward intermediates dbg [N][24] = {t, t_final, n.x, n.y, n.z, lighting,
  * mix.r, mix.g, mix.b, D_final, mask, n.l, min delta, Zw, Zb, 0, D(+x), D(-x), D(+y),
