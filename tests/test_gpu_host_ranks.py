@@ -162,3 +162,58 @@ def test_cli_ranks_1_over_rccl(tmp_path):
     line = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][-1])
     assert line["ranks"] == 1 and line["steps"] == STAGES * STEPS
     assert os.path.exists(tmp_path / "scene.json")
+
+
+def _failing_worker(rank, world, port, out_dir):
+    """Rank 0's all-reduce fails at its 5th step (an injected fault); both ranks must leave
+    rmh_train with an error -- rank 0 from the fault, rank 1 because its peer is gone -- instead of
+    rank 1 waiting in the collective forever."""
+    import sys
+    import datetime
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=60))
+    from burn_raymarching_amd import host as H
+    hip = _hip()
+    calls = {"n": 0}
+
+    def all_reduce(buf, count, stream):
+        calls["n"] += 1
+        if rank == 0 and calls["n"] == 5:
+            raise RuntimeError("injected fault")
+        assert hip.hipStreamSynchronize(stream) == 0
+        a = np.empty(count, np.float32)
+        assert hip.hipMemcpy(a.ctypes.data, buf, 4 * count, 2) == 0
+        t = torch.from_numpy(a)
+        dist.all_reduce(t)
+        assert hip.hipMemcpy(buf, t.numpy().ctypes.data, 4 * count, 1) == 0
+
+    def broadcast(buf, count, root, stream):
+        raise RuntimeError("no stage transition in this test")
+
+    def abort():  # the failing rank releases its side: its peer's pending collective then fails
+        dist.destroy_process_group()
+
+    comm = H.collective(rank, world, all_reduce, broadcast, abort=abort)
+    cfg = _cfg(H)
+    cfg.stages = 1
+    cfg.comm = ctypes.pointer(comm)
+    err = None
+    try:
+        H.train(cfg)
+    except H.HostError as e:
+        err = str(e)
+    json.dump({"rank": rank, "error": err, "calls": calls["n"]}, open(os.path.join(out_dir, f"f{rank}.json"), "w"))
+
+
+@pytest.mark.timeout(200)
+def test_failing_rank_does_not_hang_its_peer():
+    world = 2
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_failing_worker, args=(world, _free_port(), tmp), nprocs=world, join=True,
+                           start_method="spawn")
+        r = [json.load(open(os.path.join(tmp, f"f{q}.json"))) for q in range(world)]
+        assert r[0]["error"] and "all-reduce of the gradient" in r[0]["error"] and r[0]["calls"] == 5
+        assert r[1]["error"] and "all-reduce of the gradient" in r[1]["error"], r[1]

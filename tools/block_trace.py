@@ -32,14 +32,28 @@ def run(args):
     from burn_raymarching_amd import native
     from burn_raymarching_amd import render as rmr
 
+    import json
+    import numpy as np
+    sys.path.insert(0, ROOT)
+    from bench import DANGO, load_scene_json
+    if args.scene_json:
+        sc0 = load_scene_json(args.scene_json)
+        args.spheres = sc0["centers"].shape[0]
     W, H, M, S, K, V = args.width, args.height, args.spheres, args.march_steps, args.smooth_k, args.views
     rr = (0.03, 0.12) if M <= 256 else ((0.02, 0.06) if M <= 1024 else (0.01, 0.04))
-    sc0 = rmm.synthetic_scene(M, seed=0, radius_range=rr)
+    if not args.scene_json:
+        sc0 = rmm.synthetic_scene(M, seed=0, radius_range=rr)
     sc1 = rmm.synthetic_scene(M, seed=1, radius_range=rr)
-    cams = rmm.ring_cameras(max(10, V))[:V]
-    tg = rmr.render_diff_camera(cams, W, H, rmm.scene_tensors(sc1), K, S).view(-1, 3)
-    mdl = rmm.SceneModel.from_activated(sc0["centers"], sc0["colors"], sc0["radius"], sc0["light_dir"],
-                                        sc0["ambient"])
+    if args.cameras:  # the generate.rs scene through the renderer.rs kernel, as bench.py --targets dango
+        cams = [(c["origin"], c["target"], c["fov"]) for c in json.load(open(args.cameras))][:V]
+        t = [torch.tensor(DANGO[k], device="cuda") for k in ("centers", "colors", "radius")]
+        tg = rmr.render_camera(cams, W, H, *t).view(-1, 3)
+    else:
+        cams = rmm.ring_cameras(max(10, V))[:V]
+        tg = rmr.render_diff_camera(cams, W, H, rmm.scene_tensors(sc1), K, S).view(-1, 3)
+    mdl = rmm.SceneModel.from_activated(sc0["centers"], np.clip(sc0["colors"], 1e-6, 1 - 1e-6), sc0["radius"],
+                                        sc0["light_dir"], sc0["ambient"],
+                                        color_dtype="f16" if args.color_f16 else "f32")
     opt = rmm.Adam(mdl, weight_decay=1e-5, with_penalties=True)
     march = native.march_params(S, K)
     g = torch.zeros(rmm.packed_size(M), device="cuda")
@@ -141,6 +155,9 @@ def main():
     ap.add_argument("--bins", type=int, default=40)
     ap.add_argument("--out", default="")
     ap.add_argument("--load", default="", help="analyse a saved .npz instead of running")
+    ap.add_argument("--scene-json", default="", help="start scene (bench.py --scene-json; --spheres from the file)")
+    ap.add_argument("--cameras", default="", help="cameras.json poses instead of the ring (bench.py --cameras)")
+    ap.add_argument("--color-f16", action="store_true")
     args = ap.parse_args()
     tr = np.load(args.load)["trace"] if args.load else run(args)
     if args.out:

@@ -51,8 +51,9 @@ def main():
     ap.add_argument("--spheres", type=int, default=256)
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--k", type=float, default=32.0)
+    ap.add_argument("--radius-range", type=float, nargs=2, default=(0.03, 0.12))
     args = ap.parse_args()
-    sc = rmm.synthetic_scene(args.spheres, seed=0)
+    sc = rmm.synthetic_scene(args.spheres, seed=0, radius_range=tuple(args.radius_range))
     c, r = sc["centers"].astype(float), sc["radius"].astype(float)
     orders = {"given": np.arange(len(c)), "morton": morton_order(c)}
     W = H = 512
