@@ -1,0 +1,63 @@
+"""Predicted strong-scaling curve of the default bench step (80 views of 512x512 per step over N
+ranks), built from one-GPU measurements, so that the driver's 8-GPU SCALE run can be checked
+against it:
+
+    T(N) = max over ranks of the rank's train call  (profiles/*_shard_balance.json: the 80/N-view
+                                                     slices timed on one GPU, each its own launch,
+                                                     scaled to the bench's kernel time)
+         + the step's work outside the train kernel (bench line at N = 1: ms_per_step - kernel ms;
+                                                     the O(M) launches do not shrink with N)
+         + one all-reduce of the 7M+5-float [gradient | loss] over N ranks:
+             measured one-rank RCCL floor (tools/allreduce_probe.py) + a ring over xGMI modelled as
+             2 (N - 1) latency-bound hops of HOP_US each (N > 1)
+
+    value(N) = 80 * 512 * 512 / T(N) Mrays/s
+
+    python tools/predict_scaling.py --bench profiles/r05_bench.json --balance profiles/r04b_shard_balance.json \
+        --allreduce profiles/r05b_allreduce.json [--hop-us 2.5] > profiles/r05_scaling_prediction.json
+"""
+import argparse
+import json
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bench", required=True, help="the N = 1 bench line (JSON)")
+    ap.add_argument("--balance", required=True, help="tools/shard_balance.py output")
+    ap.add_argument("--allreduce", required=True, help="tools/allreduce_probe.py output")
+    ap.add_argument("--order", default="spread")
+    ap.add_argument("--hop-us", type=float, default=2.5,
+                    help="modelled latency of one xGMI ring hop of a few-KB message (no measurement on a "
+                         "one-GPU box; an assumption, stated in the output)")
+    args = ap.parse_args()
+    b = json.load(open(args.bench))
+    bal = json.load(open(args.balance))[args.order]
+    ar = json.load(open(args.allreduce))["allreduce"]
+    M = b["config"]["spheres"]
+    rays = b["config"]["rays_per_step"]
+    kern1 = b["roofline"]["kernel_ms_per_step"]
+    outside = b["ms_per_step"] - kern1
+    floor_us = ar[str(M)]["median_us"] if str(M) in ar else min(v["median_us"] for v in ar.values())
+    out = {"inputs": {"bench": args.bench, "balance": args.balance, "allreduce": args.allreduce,
+                      "kernel_ms_n1": kern1, "outside_ms": round(outside, 4), "allreduce_floor_us": floor_us,
+                      "hop_us_assumed": args.hop_us},
+           "curve": {}}
+    for n in (1, 2, 4, 8):
+        slice_ms = kern1 if n == 1 else max(bal[str(n)]["slice_ms"])
+        # the balance study timed each rank's slice as its own launch (as the rank runs it), on a
+        # scene earlier in training than the bench's timed steps: its slices are scaled by the
+        # bench's kernel time over the study's two-slice total (the same 80 views)
+        if n > 1:
+            slice_ms *= kern1 / sum(bal["2"]["slice_ms"])
+        ar_ms = 0.0 if n == 1 else (floor_us + 2 * (n - 1) * args.hop_us) * 1e-3
+        t = slice_ms + outside + ar_ms
+        out["curve"][str(n)] = {"step_ms": round(t, 4), "train_kernel_ms": round(slice_ms, 4),
+                                "allreduce_ms": round(ar_ms, 4), "mrays_s": round(rays / (t * 1e-3) / 1e6, 1)}
+    v1 = out["curve"]["1"]["mrays_s"]
+    for n in ("2", "4", "8"):
+        out["curve"][n]["efficiency"] = round(out["curve"][n]["mrays_s"] / (int(n) * v1), 3)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
