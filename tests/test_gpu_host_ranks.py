@@ -74,7 +74,7 @@ def _gloo_collective(H, rank, world, log):
     return H.collective(rank, world, all_reduce, broadcast)
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, grow=False):
     import sys
     sys.path.insert(0, ROOT)
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -84,6 +84,9 @@ def _worker(rank, world, port, out_dir):
     log = []
     comm = _gloo_collective(H, rank, world, log)
     cfg = _cfg(H)
+    if grow:  # configs[4]-style growth: every surviving sphere splits, 128 march steps, fp16 colours
+        cfg.stages, cfg.steps_per_stage, cfg.march_steps = 8, 6, 128
+        cfg.split_scale, cfg.split_move, cfg.color_f16 = 0.0, 0.0, 1
     cfg.comm = ctypes.pointer(comm)
     res, raw = H.train(cfg)
     np.save(os.path.join(out_dir, f"raw{rank}.npy"), raw)
@@ -102,6 +105,23 @@ def _free_port():
     p = s.getsockname()[1]
     s.close()
     return p
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_growth_broadcasts_large_generations():
+    """The rank-0 broadcast of the next generation at configs[4]-style growth (7 -> ~900 spheres,
+    128 march steps, fp16 colours): every stage transition broadcasts the size, then 7M'+4 raw
+    parameters; both ranks end bit-identical, past 512 spheres."""
+    world = 2
+    with tempfile.TemporaryDirectory() as tmp:
+        mp.start_processes(_worker, args=(world, _free_port(), tmp, True), nprocs=world, join=True,
+                           start_method="spawn")
+        r = [json.load(open(os.path.join(tmp, f"r{q}.json"))) for q in range(world)]
+        raw = [np.load(os.path.join(tmp, f"raw{q}.npy")) for q in range(world)]
+        assert np.array_equal(raw[0], raw[1]) and np.isfinite(raw[0]).all()
+        assert r[0]["M"] == r[1]["M"] and r[0]["M"] > 512, r[0]["M"]
+        sizes = [c for k, c in r[0]["seq"] if k == "bc" and c != 1]
+        assert len(sizes) == 7 and sizes[-1] == 7 * r[0]["M"] + 4
 
 
 @pytest.mark.timeout(300)
