@@ -521,7 +521,9 @@ def main():
     if dist is not None:
         # per-rank train-kernel and all-reduce times (sampled steps), before the max over ranks
         ar_ms = dp.collect_allreduce_ms()
-        mine = torch.tensor([kern_rank_ms, ar_ms if ar_ms is not None else -1.0], device="cuda", dtype=torch.float64)
+        # (RCCL gathers device tensors; the gloo rehearsal host tensors)
+        mine = torch.tensor([kern_rank_ms, ar_ms if ar_ms is not None else -1.0], dtype=torch.float64,
+                            device="cuda" if backend == "nccl" else "cpu")
         every_rank = [torch.zeros_like(mine) for _ in range(world)]
         dist.all_gather(every_rank, mine)
         per = torch.stack(every_rank).cpu().numpy()
