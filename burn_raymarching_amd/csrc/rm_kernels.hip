@@ -3037,6 +3037,7 @@ struct rm_context {
   rm::CamBasis* cams_pin = nullptr;         // their pinned host staging, kCamRing slots
   hipEvent_t cam_ev[32] = {};               // slot k's copy has run (kCamRing slots)
   int cam_slot = 0;
+  std::vector<rm::CamBasis> cams_shadow;    // what the device table holds (the last upload)
   float* batch = nullptr;                   // rm_train_iteration's unfused path: the drawn batch (9 floats/ray)
   float* opt_pre = nullptr;                 // rm_train_iteration: the optimizer part of the launch's extra block
   size_t batch_bytes = 0;
@@ -3458,6 +3459,23 @@ int upload_cams(rm_context* ctx, const Call& c, KArgs& a) {
       return fail(ctx, RM_ERR_OOM, "camera staging");
     for (hipEvent_t& e : ctx->cam_ev) RM_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
   }
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  RM_HIP(ctx, hipStreamIsCapturing(ctx->stream, &cap));
+  if (cap != hipStreamCaptureStatusNone) {
+    // under hipGraph capture nothing may wait or stage: the call must find its views in the device
+    // table already -- an eager call with the same views on this context uploaded them -- and the
+    // replays read that table (the caller keeps it: no call with other views on this context)
+    std::vector<CamBasis> want(c.views);
+    for (int v = 0; v < c.views; ++v)
+      if ((rc = make_basis(ctx, c.cams[v], c.W, c.H, want[v])) != RM_OK) return rc;
+    if (ctx->cams_shadow.size() != want.size() ||
+        std::memcmp(ctx->cams_shadow.data(), want.data(), sizeof(CamBasis) * want.size()) != 0)
+      return fail(ctx, RM_ERR_UNSUPPORTED,
+                  "a captured call of %d views reads the context's camera table: run the same call once before "
+                  "the capture", c.views);
+    a.cams_dev = ctx->cams_dev;
+    return RM_OK;
+  }
   const int slot = ctx->cam_slot;
   ctx->cam_slot = (slot + 1) % kCamRing;
   RM_HIP(ctx, hipEventSynchronize(ctx->cam_ev[slot]));
@@ -3466,6 +3484,7 @@ int upload_cams(rm_context* ctx, const Call& c, KArgs& a) {
     if ((rc = make_basis(ctx, c.cams[v], c.W, c.H, pin[v])) != RM_OK) return rc;
   RM_HIP(ctx, hipMemcpyAsync(ctx->cams_dev, pin, sizeof(CamBasis) * c.views, hipMemcpyHostToDevice, ctx->stream));
   RM_HIP(ctx, hipEventRecord(ctx->cam_ev[slot], ctx->stream));
+  ctx->cams_shadow.assign(pin, pin + c.views);
   a.cams_dev = ctx->cams_dev;
   return RM_OK;
 }

@@ -1,7 +1,8 @@
 """hipGraph capture of a training step (raymarch.h, "hipGraph capture of a training step"): a step
 of bench.py's shape -- rm_train_step_camera (records, origin steps, train kernel, reduction) then
 rm_optimizer_step -- captured once with torch.cuda.CUDAGraph over the rm_* calls and replayed,
-gives the eager steps' results bit for bit: the per-step scalars (compute_loss's progress, Adam's
+gives the eager steps' results bit for bit (also for a call of more than 16 views, whose camera
+bases the captured call reads from the context's device table): the per-step scalars (compute_loss's progress, Adam's
 step) come from a device record the optimizer advances (rm_bind_step_scalars), and the cost-ordered
 dispatch rotates its list sets on the device (the replayed launches keep using the previous step's
 cost order)."""
@@ -32,7 +33,7 @@ def _setup(torch, rmm, rmr, native, m, w, views, steps, order):
 
 
 @pytest.mark.parametrize("order", ["cost", "static"])
-@pytest.mark.parametrize("m,w,views,steps", [(64, 128, 4, 24), (300, 64, 2, 64)])
+@pytest.mark.parametrize("m,w,views,steps", [(64, 128, 4, 24), (300, 64, 2, 64), (40, 32, 20, 16)])
 def test_graph_replay_equals_eager(order, m, w, views, steps):
     import torch
     from burn_raymarching_amd import model as rmm

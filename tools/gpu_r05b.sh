@@ -9,7 +9,6 @@ bash tools/gpu_iter.sh r05b tests && \
 timeout -k 10 200 python bench.py $C2 --graph off > $O/c2_eager.json 2> $O/c2_eager.err && \
 timeout -k 10 200 python bench.py $C2 --graph on > $O/c2_graph.json 2> $O/c2_graph.err && \
 timeout -k 10 200 python bench.py $C2 --graph off > $O/c2_eager2.json 2>> $O/c2_eager.err && \
-timeout -k 10 200 python bench.py --cpu-baseline off --graph on > $O/metric_graph.json 2> $O/metric_graph.err && \
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof_c2_graph -o run -- python3 bench.py $C2 --graph on --aux-steps 0 > $O/prof_c2_graph.log 2>&1 && \
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/$O/prof_c2_eager -o run -- python3 bench.py $C2 --graph off --aux-steps 0 > $O/prof_c2_eager.log 2>&1 && \
 timeout -k 10 120 python tools/allreduce_probe.py > $O/allreduce.json 2> $O/allreduce.err && \
@@ -17,7 +16,8 @@ RM_LIB_PATH=burn_raymarching_amd/lib/var/trace.so timeout -k 10 200 python tools
   --views 1 --warm 2 --bins 20 --color-f16 --scene-json profiles/r05a_grown_scene_4096.json \
   --cameras tests/golden/cameras.json --out $O/bt_c5g.npz > $O/bt_c5g.txt 2>&1 && \
 RM_LIB_PATH=burn_raymarching_amd/lib/var/trace.so timeout -k 10 200 python tools/block_trace.py --spheres 4096 \
-  --march-steps 128 --views 1 --warm 2 --bins 20 --out $O/bt_c5.npz > $O/bt_c5.txt 2>&1
+  --march-steps 128 --views 1 --warm 2 --bins 20 --out $O/bt_c5.npz > $O/bt_c5.txt 2>&1 && \
+timeout -k 10 200 python bench.py --cpu-baseline off --graph on > $O/metric_graph.json 2> $O/metric_graph.err
 rc=$?
 for f in c2_eager c2_graph c2_eager2 metric_graph; do
   python3 -c "import json,sys; d=json.load(open('$O/$f.json')); r=d['roofline']; print(sys.argv[1], d['value'], d['ms_per_step'], d['ms_per_step_median'], r['kernel_ms_per_step'], r['frac'])" $f
