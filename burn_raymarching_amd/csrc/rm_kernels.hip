@@ -69,6 +69,14 @@
 #ifndef RM_ORDER_CLASSES
 #define RM_ORDER_CLASSES 16  // cost classes of the cost-ordered dispatch (order_append)
 #endif
+// ints between the three list sets' class counts and before the turn word: each on cache lines of
+// its own (every block of a launch reads the turn and the previous set's counts while the blocks'
+// appends hit the current set's counts with atomics; sharing a 128-byte line made every launch
+// that appended to the set next to the turn word 50 % slower at C2: tools/order_probe.py)
+#ifndef RM_ORDER_CNT_STRIDE
+#define RM_ORDER_CNT_STRIDE 64
+#endif
+static_assert(RM_ORDER_CNT_STRIDE >= RM_ORDER_CLASSES && RM_ORDER_CNT_STRIDE % 32 == 0, "128-byte lines per set");
 #ifndef RM_BWD_COMB_BUFS
 #define RM_BWD_COMB_BUFS 1  // transposed backward: combine buffers (1 keeps the block's LDS <= 32 KB)
 #endif
@@ -1146,13 +1154,13 @@ __device__ __forceinline__ OrderSets order_sets(const KArgs& a) {
     constexpr long long kSet = (long long)RM_ORDER_CLASSES * kMaxBlocksPerLaunch;
     if (o.list_r != nullptr) {
       o.list_r += r * kSet;
-      o.cnt_r += r * RM_ORDER_CLASSES;
+      o.cnt_r += r * RM_ORDER_CNT_STRIDE;
     }
     if (o.list_w != nullptr) {
       o.list_w += w * kSet;
-      o.cnt_w += w * RM_ORDER_CLASSES;
+      o.cnt_w += w * RM_ORDER_CNT_STRIDE;
     }
-    if (o.cnt_z != nullptr) o.cnt_z += z * RM_ORDER_CLASSES;
+    if (o.cnt_z != nullptr) o.cnt_z += z * RM_ORDER_CNT_STRIDE;
   }
   return o;
 }
@@ -3684,9 +3692,10 @@ int run(rm_context* ctx, const Call& c) {
       constexpr int kCls = RM_ORDER_CLASSES;
       if (!ctx->olist) {
         RM_HIP(ctx, hipMalloc(&ctx->olist, sizeof(int) * 3 * kCls * kMaxBlocksPerLaunch));
-        RM_HIP(ctx, hipMalloc(&ctx->ocnt, sizeof(int) * (3 * kCls + 1)));  // + the turn word
-        RM_HIP(ctx, hipMemsetAsync(ctx->ocnt, 0, sizeof(int) * (3 * kCls + 1), ctx->stream));
-        ctx->oturn = ctx->ocnt + 3 * kCls;
+        // the three sets' counts, then the turn word, RM_ORDER_CNT_STRIDE ints apart
+        RM_HIP(ctx, hipMalloc(&ctx->ocnt, sizeof(int) * 4 * RM_ORDER_CNT_STRIDE));
+        RM_HIP(ctx, hipMemsetAsync(ctx->ocnt, 0, sizeof(int) * 4 * RM_ORDER_CNT_STRIDE, ctx->stream));
+        ctx->oturn = ctx->ocnt + 3 * RM_ORDER_CNT_STRIDE;
       }
       // three list sets in rotation: the previous launch's (read), this launch's (appended;
       // cleared by the previous launch) and the next launch's (cleared by this one); which is which
@@ -3856,11 +3865,12 @@ int rm_debug_order_counts(rm_context* ctx, int32_t* counts, int32_t capacity, in
   if (classes) *classes = kCls;
   if (counts && capacity < 3 * kCls) return fail(ctx, RM_ERR_INVALID_ARG, "counts needs %d entries", 3 * kCls);
   RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  std::vector<int> host(3 * kCls + 1, 0);  // the counts and the device turn word
+  std::vector<int> host(4 * RM_ORDER_CNT_STRIDE, 0);  // the sets' counts and the device turn word
   if (ctx->ocnt) RM_HIP(ctx, hipMemcpy(host.data(), ctx->ocnt, sizeof(int) * host.size(), hipMemcpyDeviceToHost));
-  if (next_set) *next_set = host[3 * kCls];
+  if (next_set) *next_set = host[3 * RM_ORDER_CNT_STRIDE];
   if (counts)
-    for (int i = 0; i < 3 * kCls; ++i) counts[i] = host[i];
+    for (int st = 0; st < 3; ++st)
+      for (int c = 0; c < kCls; ++c) counts[st * kCls + c] = host[st * RM_ORDER_CNT_STRIDE + c];
   return RM_OK;
 }
 
