@@ -73,10 +73,17 @@
 // its own (every block of a launch reads the turn and the previous set's counts while the blocks'
 // appends hit the current set's counts with atomics; sharing a 128-byte line made every launch
 // that appended to the set next to the turn word 50 % slower at C2: tools/order_probe.py)
-#ifndef RM_ORDER_CNT_STRIDE
-#define RM_ORDER_CNT_STRIDE 64
+#ifndef RM_ORDER_CLS_STRIDE
+#define RM_ORDER_CLS_STRIDE 1  // ints between a set's class counts (32: each class on a line of its own)
 #endif
-static_assert(RM_ORDER_CNT_STRIDE >= RM_ORDER_CLASSES && RM_ORDER_CNT_STRIDE % 32 == 0, "128-byte lines per set");
+#ifndef RM_ORDER_CNT_STRIDE
+#define RM_ORDER_CNT_STRIDE (RM_ORDER_CLASSES * RM_ORDER_CLS_STRIDE > 64 ? RM_ORDER_CLASSES * RM_ORDER_CLS_STRIDE : 64)
+#endif
+static_assert(RM_ORDER_CNT_STRIDE >= RM_ORDER_CLASSES * RM_ORDER_CLS_STRIDE && RM_ORDER_CNT_STRIDE % 32 == 0,
+              "128-byte lines per set");
+#ifndef RM_RED_ARR_STRIDE
+#define RM_RED_ARR_STRIDE 1  // unsigneds between rm_reduce_partials' arrival counters (32: a line each)
+#endif
 #ifndef RM_BWD_COMB_BUFS
 #define RM_BWD_COMB_BUFS 1  // transposed backward: combine buffers (1 keeps the block's LDS <= 32 KB)
 #endif
@@ -1193,7 +1200,7 @@ __device__ __forceinline__ long long ray_block(const KArgs& a, int* cls = nullpt
     int tot = 0, cb = -1, base = 0;
 #pragma unroll
     for (int c = 0; c < RM_ORDER_CLASSES; ++c) {
-      const int n = os.cnt_r[c];
+      const int n = os.cnt_r[c * RM_ORDER_CLS_STRIDE];
       if (cb < 0 && b < tot + n) {
         cb = c;
         base = tot;
@@ -1216,7 +1223,7 @@ __device__ __forceinline__ void order_append(const KArgs& a, long long blk, int 
   const float cls_scale = (float)kCls / (float)((a.split ? 1 : kWaves) * (a.steps + kPostCost) + 1);
   const int c = kCls - 1 - (int)fminf((float)cost * cls_scale, (float)(kCls - 1));
   const OrderSets os = order_sets(a);
-  const int idx = atomicAdd(os.cnt_w + c, 1);
+  const int idx = atomicAdd(os.cnt_w + c * RM_ORDER_CLS_STRIDE, 1);
   // counts left uncleared (a failed launch in the rotation) overrun the total, and ray_block
   // then falls back to the static order: never write past the list
   if (idx < kMaxBlocksPerLaunch) os.list_w[c * kMaxBlocksPerLaunch + idx] = (int)blk;
@@ -1411,7 +1418,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   // ---- escape skip (RM_MARCH_SKIP_ESCAPED): a block whose rays all provably leave the scene
   // (rm_escape_kernel) gets out = 0 and zero gradients without marching -- exactly what the full
   // computation yields for them, since their silhouette mask is 0 in f32 (see escapes()).
-  if (a.ocnt_z != nullptr && blockIdx.x == 0 && tid < RM_ORDER_CLASSES) order_sets(a).cnt_z[tid] = 0;
+  if (a.ocnt_z != nullptr && blockIdx.x == 0 && tid < RM_ORDER_CLASSES) order_sets(a).cnt_z[tid * RM_ORDER_CLS_STRIDE] = 0;
   if (a.esc_flags != nullptr && a.esc_flags[blk]) {
     if (a.stats != nullptr && tid == 0) atomicAdd(a.stats, 1ull);
     if (a.ocnt_w != nullptr && tid == 0) order_append(a, blk, 0);
@@ -2496,7 +2503,8 @@ __global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restric
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (tid == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(arrivals + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned prev = __hip_atomic_fetch_add(arrivals + blockIdx.x * RM_RED_ARR_STRIDE, 1u, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
     last = prev == gridDim.y - 1 ? 1 : 0;
   }
   __syncthreads();
@@ -2507,7 +2515,7 @@ __global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restric
   }
   __syncthreads();
   finalize_block(S, (int)gridDim.y, M, Mpad, f, tot);
-  if (tid == 0) __hip_atomic_store(arrivals + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) __hip_atomic_store(arrivals + blockIdx.x * RM_RED_ARR_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Pass 2 for the 256 columns of pass-1 column block blockIdx.x, by the block of that column block
@@ -3137,7 +3145,7 @@ bool env_is(const char* name, char v) {
 
 int pad_spheres(int M) { return (M + kSphereAlign - 1) / kSphereAlign * kSphereAlign; }
 // column blocks of the reduction at the largest scene (RM_MAX_SPHERES): its arrival counters
-constexpr int kRedArrivals = (RM_MAX_SPHERES * 8 + 8 + 255) / 256;
+constexpr int kRedArrivals = (RM_MAX_SPHERES * 8 + 8 + 255) / 256 * RM_RED_ARR_STRIDE;
 
 // Ray blocks per per-ray launch: kMaxBlocksPerLaunch, or less with the environment variable
 // RM_MAX_BLOCKS_PER_LAUNCH (tests use it to exercise the sub-launch split at small sizes).
@@ -3870,7 +3878,7 @@ int rm_debug_order_counts(rm_context* ctx, int32_t* counts, int32_t capacity, in
   if (next_set) *next_set = host[3 * RM_ORDER_CNT_STRIDE];
   if (counts)
     for (int st = 0; st < 3; ++st)
-      for (int c = 0; c < kCls; ++c) counts[st * kCls + c] = host[st * RM_ORDER_CNT_STRIDE + c];
+      for (int c = 0; c < kCls; ++c) counts[st * kCls + c] = host[st * RM_ORDER_CNT_STRIDE + c * RM_ORDER_CLS_STRIDE];
   return RM_OK;
 }
 

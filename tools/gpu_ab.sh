@@ -3,7 +3,7 @@
 # "lib:<name>" (the kernel library burn_raymarching_amd/lib/var/<name>.so, built with
 # tools/build_variant.sh). Configs: m (metric, strong default), m10 (10 views per GPU), m16 (the default's
 # 80 views in calls of 16), ms / ms8 (the
-# default's calls on 4 streams, 16 / 8 views per call), c2, c3,
+# default's calls on 4 streams, 16 / 8 views per call), c2, c2cj (C2 on the cameras.json poses), c3,
 # c4, c5, c5r1 (C5 on a fixed view), c5s (C5 on a 64x64 view).
 #   CONFIGS="m c5" ROUNDS=2 bash tools/gpu_ab.sh default "RM_X=1" lib:trace
 set -o pipefail
@@ -29,6 +29,7 @@ for r in $(seq 1 $ROUNDS); do
         ms) args="--streams 4 --steps 10" ;;
         ms8) args="--streams 4 --views-per-call 8 --steps 10" ;;
         c2) args="--width 256 --height 256 --spheres 64 --views-per-gpu 10 --steps 20" ;;
+        c2cj) args="--width 256 --height 256 --spheres 64 --views-per-gpu 10 --steps 40 --cameras tests/golden/cameras.json --targets files" ;;
         c3) args="--march-steps 64 --views-per-gpu 10 --steps 10" ;;
         c4) args="--width 1024 --height 1024 --spheres 1024 --march-steps 64 --views-per-gpu 4 --steps 4 --warmup 2" ;;
         c5) args="--spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 4 --warmup 2" ;;
