@@ -74,7 +74,10 @@
 // appends hit the current set's counts with atomics; sharing a 128-byte line made every launch
 // that appended to the set next to the turn word 50 % slower at C2: tools/order_probe.py)
 #ifndef RM_ORDER_CLS_STRIDE
-#define RM_ORDER_CLS_STRIDE 1  // ints between a set's class counts (32: each class on a line of its own)
+// ints between a set's class counts: each class on a 128-byte line of its own, as the reduction's
+// arrival counters below (both: C2cj 4348-4404 vs 4305-4315 Mrays/s with neither, the metric
+// equal; tools/gpu_ab.sh, profiles/r05e_ab.txt)
+#define RM_ORDER_CLS_STRIDE 32
 #endif
 #ifndef RM_ORDER_CNT_STRIDE
 #define RM_ORDER_CNT_STRIDE (RM_ORDER_CLASSES * RM_ORDER_CLS_STRIDE > 64 ? RM_ORDER_CLASSES * RM_ORDER_CLS_STRIDE : 64)
@@ -82,7 +85,7 @@
 static_assert(RM_ORDER_CNT_STRIDE >= RM_ORDER_CLASSES * RM_ORDER_CLS_STRIDE && RM_ORDER_CNT_STRIDE % 32 == 0,
               "128-byte lines per set");
 #ifndef RM_RED_ARR_STRIDE
-#define RM_RED_ARR_STRIDE 1  // unsigneds between rm_reduce_partials' arrival counters (32: a line each)
+#define RM_RED_ARR_STRIDE 32  // unsigneds between rm_reduce_partials' arrival counters: a 128-byte line each
 #endif
 #ifndef RM_BWD_COMB_BUFS
 #define RM_BWD_COMB_BUFS 1  // transposed backward: combine buffers (1 keeps the block's LDS <= 32 KB)
