@@ -64,4 +64,5 @@ run C4s 1024x1024_M1024_S64_V32 --width 1024 --height 1024 --spheres 1024 --marc
 run C5 512x512_M4096_S128_V1 --spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 6 --warmup 2 && \
 run C5f16 512x512_M4096_S128_V1_c16 --spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 6 --warmup 2 --color-dtype f16 && \
 run k5 512x512_M256_S32_V80_k5 --smooth-k 5 --steps 10 && \
-python3 tools/configs_summary.py $O profiles/${TAG}_configs.json && cp profiles/${TAG}_configs.json $O/
+python3 tools/configs_summary.py $O profiles/${TAG}_configs.json && cp profiles/${TAG}_configs.json $O/ && \
+{ [ -z "$PMC" ] || cp profiles/${TAG}_pmc_traffic.json profiles/${TAG}_pmc_sq.json $O/; }
