@@ -4,7 +4,7 @@
 # tools/build_variant.sh). Configs: m (metric, strong default), m10 (10 views per GPU), m16 (the default's
 # 80 views in calls of 16), ms / ms8 (the
 # default's calls on 4 streams, 16 / 8 views per call), c2, c2cj (C2 on the cameras.json poses), c3,
-# c4, c5, c5r1 (C5 on a fixed view), c5s (C5 on a 64x64 view).
+# c4, c5, c5r1 (C5 on a fixed view), c5s (C5 on a 64x64 view), c5g (configs[4] on the grown model).
 #   CONFIGS="m c5" ROUNDS=2 bash tools/gpu_ab.sh default "RM_X=1" lib:trace
 set -o pipefail
 mkdir -p gpurun_out/ab
@@ -35,6 +35,7 @@ for r in $(seq 1 $ROUNDS); do
         c5) args="--spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 4 --warmup 2" ;;
         c5r1) args="--spheres 4096 --march-steps 128 --views-per-gpu 1 --ring 1 --steps 4 --warmup 2" ;;
         c5s) args="--width 64 --height 64 --spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 4 --warmup 2" ;;
+        c5g) args="--march-steps 128 --views-per-gpu 1 --steps 6 --warmup 2 --color-dtype f16 --cameras tests/golden/cameras.json --targets dango --scene-json profiles/r05a_grown_scene_4096.json" ;;
       esac
       env $envs timeout -k 10 200 python bench.py --cpu-baseline off $args > gpurun_out/ab/${c}_v${i}_$r.json \
         2> gpurun_out/ab/${c}_v${i}_$r.err || { tail -5 gpurun_out/ab/${c}_v${i}_$r.err; exit 1; }
