@@ -39,7 +39,13 @@ def main():
             for row in rows:
                 kern[row["Name"][:90]] = {"calls": int(row["Calls"]), "avg_us": round(float(row["AverageNs"]) / 1e3, 2)}
             entry["rocprof_kernels"] = kern
-            train = next((v for k, v in kern.items() if "rm_ray_kernel<2, true" in k), None)
+            # the camera-mode train kernel: rm_ray_kernel<2, true, SPLIT> and a split launch's
+            # continuation kernel rm_cont_kernel<2, true> (summed)
+            tk = [v for k, v in kern.items() if "rm_ray_kernel<2, true" in k or "rm_cont_kernel<2, true" in k]
+            train = None
+            if tk:
+                calls = sum(v["calls"] for v in tk)
+                train = {"calls": calls, "avg_us": round(sum(v["avg_us"] * v["calls"] for v in tk) / calls, 2)}
             opt = next((v for k, v in kern.items() if "rm_optimizer" in k), None)
             if train:
                 # steps = optimizer calls (one per step); a split launch with a continuation runs the
@@ -51,7 +57,8 @@ def main():
                 # the per-step kernels besides the train kernel (one-off setup launches, e.g. the
                 # target render, run fewer times than there are steps)
                 other = sum(v["avg_us"] * v["calls"] for k, v in kern.items()
-                            if ("rm::" in k or "rm_optimizer" in k) and "rm_ray_kernel" not in k and v["calls"] >= steps)
+                            if ("rm::" in k or "rm_optimizer" in k) and "rm_ray_kernel" not in k and "rm_cont_kernel" not in k
+                            and v["calls"] >= steps)
                 entry["rocprof_other_us_per_step"] = round(other / steps, 2)
         res[name] = entry
     json.dump(res, open(out, "w"), indent=1)

@@ -27,6 +27,11 @@ import os
 import sys
 
 KERNEL = "rm_ray_kernel<2, true"  # <2, true, SPLIT>: the camera-mode train kernel
+KERNELS = (KERNEL, "rm_cont_kernel<2, true")  # ... and a split launch's continuation kernel
+
+
+def is_train(name):
+    return any(k in name for k in KERNELS)
 TRANS_CYCLES = 8.6    # cycles per transcendental wave-instruction per SIMD (r01_valu_rates.txt)
 OTHER_CYCLES = 4.0    # other VALU: fma 2.96, add 3.56, max 4.45, packed fma 5.02 (r01_valu_rates.txt)
 SIMDS = 1024          # 256 CUs x 4 SIMDs
@@ -43,7 +48,7 @@ def rows(path, suffix):
 def counters(path):
     vals = {}
     for r in rows(path, "counter_collection.csv"):
-        if KERNEL not in r["Kernel_Name"]:
+        if not is_train(r["Kernel_Name"]):
             continue
         vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in vals.items()}, max((len(v) for v in vals.values()), default=0)
@@ -51,7 +56,7 @@ def counters(path):
 
 def duration_ns(path):
     d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows(path, "kernel_trace.csv")
-         if KERNEL in r["Kernel_Name"]]
+         if is_train(r["Kernel_Name"])]
     return sum(d) / len(d) if d else None
 
 

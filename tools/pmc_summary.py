@@ -55,7 +55,8 @@ def main():
     wf = calib["write_rec_factor"] if calib else 1.0
     f = per_kernel(fetch_dir, "FETCH_SIZE")
     w = per_kernel(write_dir, "WRITE_SIZE")
-    names = [k for k in f if "rm_ray_kernel<2, true" in k]  # camera-mode train kernel (split or not)
+    # camera-mode train kernel (split or not) and a split launch's continuation kernel
+    names = [k for k in f if "rm_ray_kernel<2, true" in k or "rm_cont_kernel<2, true" in k]
     if not names:
         raise SystemExit("train kernel not found in the counter CSVs")
     fv = [x for k in names for x in f[k]]
