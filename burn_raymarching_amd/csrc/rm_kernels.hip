@@ -117,6 +117,9 @@ constexpr long long kSplitMaxRaysWide = 1048576;
 #define RM_SPLIT_MIN_WAVES 3  // register budget of the split kernels (waves per SIMD): 3 = 168 VGPRs, no
                               // spills (4: 128 VGPRs, 4-12 VGPR spills, 20 B/lane scratch; C5 equal either way)
 #endif
+#ifndef RM_CONT_MIN_WAVES
+#define RM_CONT_MIN_WAVES RM_SPLIT_MIN_WAVES  // register budget of the split continuation kernel
+#endif
 constexpr int kSplitWaves = RM_SPLIT_WAVES;  // waves per 64-ray block of the split march (2 or 4)
 static_assert(kSplitWaves == 2 || kSplitWaves == 4, "split blocks have 2 or 4 waves");
 constexpr long long kSplitMaxRays = 262144;
@@ -1341,7 +1344,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a);
 // a.btrace[kTraceWords * (blockIdx.x * kWaves + wave) ...] (tools/block_trace.py).
 // SPLIT: the split march (RM_MARCH_SPLIT, KArgs::split).
 template <int MODE, bool CAM, bool SPLIT>
-__global__ __launch_bounds__(kBlock, SPLIT ? RM_SPLIT_MIN_WAVES : kMinWavesPerSimd) void rm_ray_kernel(const KArgs a) {
+__device__ __forceinline__ void ray_entry(const KArgs& a) {
 #ifdef RM_BLOCK_TRACE
   const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
   ray_body<MODE, CAM, SPLIT>(a);
@@ -1358,6 +1361,16 @@ __global__ __launch_bounds__(kBlock, SPLIT ? RM_SPLIT_MIN_WAVES : kMinWavesPerSi
 #else
   ray_body<MODE, CAM, SPLIT>(a);
 #endif
+}
+template <int MODE, bool CAM, bool SPLIT>
+__global__ __launch_bounds__(kBlock, SPLIT ? RM_SPLIT_MIN_WAVES : kMinWavesPerSimd) void rm_ray_kernel(const KArgs a) {
+  ray_entry<MODE, CAM, SPLIT>(a);
+}
+// The split continuation launch (KArgs::cont_resume > 0) as its own kernel: the same code at the
+// register budget RM_CONT_MIN_WAVES (waves per SIMD), so that more of its blocks are resident at once.
+template <int MODE, bool CAM>
+__global__ __launch_bounds__(kBlock, RM_CONT_MIN_WAVES) void rm_cont_kernel(const KArgs a) {
+  ray_entry<MODE, CAM, true>(a);
 }
 
 // Split march (SPLIT): a block takes 64 rays (one 8x8 quadrant of a 16x16 tile in camera mode)
@@ -3448,6 +3461,13 @@ void launch_escape(bool cam, dim3 grid, hipStream_t st, const KArgs& a, int* fla
 }
 
 template <int MODE>
+void launch_cont(bool cam, dim3 grid, size_t lds, hipStream_t st, const KArgs& a, hipEvent_t ev0, hipEvent_t ev1) {
+  const dim3 blk(64 * kSplitWaves);
+  if (cam) hipExtLaunchKernelGGL((rm_cont_kernel<MODE, true>), grid, blk, (uint32_t)lds, st, ev0, ev1, 0u, a);
+  else hipExtLaunchKernelGGL((rm_cont_kernel<MODE, false>), grid, blk, (uint32_t)lds, st, ev0, ev1, 0u, a);
+}
+
+template <int MODE>
 void launch_ray(bool cam, bool split, dim3 grid, size_t lds, hipStream_t st, const KArgs& a, hipEvent_t ev0,
                 hipEvent_t ev1) {
   // With timing on, the start/stop timestamps come from the kernel's own dispatch packet
@@ -3799,8 +3819,8 @@ int run(rm_context* ctx, const Call& c) {
         b.ocnt_r = nullptr;
         hipEvent_t e0, e1;
         if ((rc = next_events(ctx, e0, e1)) != RM_OK) return rc;
-        if (c.mode == kBwd) launch_ray<kBwd>(c.cam, true, grid, lds, ctx->stream, b, e0, e1);
-        else launch_ray<kTrain>(c.cam, true, grid, lds, ctx->stream, b, e0, e1);
+        if (c.mode == kBwd) launch_cont<kBwd>(c.cam, grid, lds, ctx->stream, b, e0, e1);
+        else launch_cont<kTrain>(c.cam, grid, lds, ctx->stream, b, e0, e1);
         RM_HIP(ctx, hipGetLastError());
       }
     }

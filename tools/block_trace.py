@@ -126,6 +126,14 @@ def analyse(tr, bins=40, steps=0):
         live = tp > tm  # waves that ran the post-march forward (and the backward)
         print(f"live waves {int(live.sum())} of {len(tr)}; march steps run: mean {run_steps.mean():.1f}, "
               f"live mean {run_steps[live].mean() if live.any() else 0:.1f}")
+        # where the waves' time goes, summed over all waves (wall time of each wave, so a phase's
+        # share includes its SIMD sharing: a proxy for its share of the launch's issue)
+        m_all = np.clip(np.where(live, tm, e) - s, 0, None)
+        p_all = np.where(live, tp - tm, 0.0)
+        b_all = np.where(live, e - tp, 0.0)
+        tot = m_all.sum() + p_all.sum() + b_all.sum()
+        print(f"summed wave time: march {m_all.sum() / tot:.3f}, post-march forward {p_all.sum() / tot:.3f}, "
+              f"backward {b_all.sum() / tot:.3f} (of {tot / 1e3:.1f} wave-ms)")
         order = np.argsort(-dur)[:12]
         print(" slowest waves: total  march  post  bwd (us)  steps  us/step  SIMD-sharing"
               + ("  paths(none f/c, fixed f/c, vector)  lse-cycles/step  march-cycles/step" if tr.shape[1] >= 12 else ""))
