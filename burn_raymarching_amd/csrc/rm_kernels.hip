@@ -60,6 +60,9 @@
 #ifndef RM_MARCH_BUFLOAD
 #define RM_MARCH_BUFLOAD 1  // matrix-core fragments by buffer loads (0: global loads)
 #endif
+#ifndef RM_MFMA32
+#define RM_MFMA32 0  // the march's matrix-core tiles as v_mfma_f32_32x32x16_bf16 (32 spheres x 32 rays)
+#endif
 #ifndef RM_CYCLE_MAX
 #define RM_CYCLE_MAX 2  // longest period (2..4) the march's cycle exit detects (3, 4: no measurable gain)
 #endif
@@ -405,9 +408,8 @@ __device__ __forceinline__ void split3(float x, unsigned& h1, unsigned& h2, unsi
 __device__ __forceinline__ unsigned pack2(unsigned lo16, unsigned hi16) { return lo16 | (hi16 << 16); }
 constexpr unsigned kBf16One = 0x3F80u;
 
-// sphere-side fragment of lane l for row block rb (rm_prep_kernel)
-__device__ __forceinline__ uint4 mfma_a_frag(const KArgs& a, int rb, int l) {
-  const int j = 16 * rb + (l & 15), g = l >> 4;
+// sphere-side fragment: K slice g (8 bf16) of sphere j (rm_prep_kernel)
+__device__ __forceinline__ uint4 mfma_a_slice(const KArgs& a, int j, int g) {
   const float kappa = a.k * kLog2e, k2 = kappa * kappa;
   float cx, cy, cz;
   if (j < a.M) {
@@ -428,6 +430,30 @@ __device__ __forceinline__ uint4 mfma_a_frag(const KArgs& a, int rb, int l) {
   if (g == 2) return make_uint4(pack2(x[2], x[2]), pack2(0u, y[2]), pack2(y[2], 0u), pack2(z[2], z[2]));
   return make_uint4(pack2(z[0], z[1]), pack2(kBf16One, kBf16One), pack2(kBf16One, C[0]), pack2(C[1], C[2]));
 }
+// Element e of the tile array: v_mfma_f32_16x16x32_bf16 -- row block rb = e / 64 of 16 spheres,
+// lane l = e % 64 holds sphere 16 rb + (l & 15), slice l >> 4; RM_MFMA32 (v_mfma_f32_32x32x16_bf16,
+// two per 32 spheres: K halves m = 0, 1) -- block e / 128 of 32 spheres, m = (e / 64) & 1, lane l
+// holds sphere 32 rb + (l & 31), slice 2 m + (l >> 5). The same bytes per sphere either way.
+__device__ __forceinline__ uint4 mfma_a_frag(const KArgs& a, int e) {
+  const int l = e & 63;
+#if RM_MFMA32
+  return mfma_a_slice(a, 32 * (e >> 7) + (l & 31), 2 * ((e >> 6) & 1) + (l >> 5));
+#else
+  return mfma_a_slice(a, 16 * (e >> 6) + (l & 15), l >> 4);
+#endif
+}
+// Sphere of weight slot e (per 16 spheres 32 slots: 16 unshifted | 16 fixed-shift weights in sphere
+// order; RM_MFMA32: per 32 spheres 64 slots, 32 | 32, slot h * 16 + 4 i + v of a half is sphere
+// 8 i + 4 h + v of the block -- the 32x32 result rows of lane half h)
+__device__ __forceinline__ int mfma_w_sphere(int e) {
+#if RM_MFMA32
+  const int x = e & 31;
+  return 32 * (e >> 6) + 8 * ((x >> 2) & 3) + 4 * (x >> 4) + (x & 3);
+#else
+  return 16 * (e >> 5) + (e & 15);
+#endif
+}
+__device__ __forceinline__ bool mfma_w_fixed(int e) { return (e & (RM_MFMA32 ? 32 : 16)) != 0; }
 
 // hdr[4..7] = the bounding sphere (c, R) of scene_bound, for the march's escape test, and its
 // distance thresholds T(n), n < kEscTab: a receding ray at distance d from c with n march steps
@@ -563,12 +589,12 @@ __global__ __launch_bounds__(256) void rm_prep_kernel(const KArgs a0, float4* __
   uint4* At = reinterpret_cast<uint4*>(tiles);
   float* Wt = reinterpret_cast<float*>(At + (size_t)nrb * 64);
 #ifndef RM_DBG_NO_TILES
-  for (int e = blockIdx.x * nt + threadIdx.x; e < nrb * 64; e += gridDim.x * nt) At[e] = mfma_a_frag(a, e >> 6, e & 63);
+  for (int e = blockIdx.x * nt + threadIdx.x; e < nrb * 64; e += gridDim.x * nt) At[e] = mfma_a_frag(a, e);
 #endif
   for (int e = blockIdx.x * nt + threadIdx.x; e < nrb * 32; e += gridDim.x * nt) {
-    const int j = 16 * (e >> 5) + (e & 15);
+    const int j = mfma_w_sphere(e);
     const float krj = j < a.M ? kappa * a.radius[j] : 0.0f;
-    Wt[e] = j >= a.M ? 0.0f : ((e & 16) ? fexp2(krj - kr_first) : fexp2(krj));
+    Wt[e] = j >= a.M ? 0.0f : (mfma_w_fixed(e) ? fexp2(krj - kr_first) : fexp2(krj));
   }
   header_reduce(rmin, rmax, spread, gridDim.x == 1 ? hdr : hdr + (size_t)(1 + blockIdx.x) * kRecHeader);
 #ifndef RM_DBG_NO_BOUND
@@ -795,6 +821,139 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
   return own;
 }
 
+#if RM_MFMA32
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+// lse_mfma with v_mfma_f32_32x32x16_bf16: per 32 spheres and 32 rays two MFMAs (K halves: slices
+// 0-1 with B = Sa, slices 2-3 with B = Sa / Sb by lane half), half the matrix-core instructions
+// of 16x16x32 per evaluation (each holds the SIMD's vector issue for 8 cycles). Lane (r, h) =
+// (l & 31, l >> 5) gets, per column block cb, 16 results of ray 32 cb + r: rows (i & 3) + 8 (i >> 2)
+// + 4 h (mfma_w_sphere's slot order); the two halves of a ray meet in one v_permlane32_swap.
+#define RM_M32_CONSUME_BODY                                          \
+  _Pragma("unroll") for (int v = 0; v < 4; ++v) {                     \
+    float q = D[4 * i + v];                                            \
+    if constexpr (CLAMP) q = qclamp(q, QMIN);                          \
+    const float rho = fsqrt(q);                                        \
+    acc[cb] = fmaf(wv[v], fexp2(FIXED ? S[cb] - rho : -rho), acc[cb]); \
+  }
+template <bool CLAMP, bool FIXED, bool BUF = (RM_MARCH_BUFLOAD != 0)>
+__device__ __forceinline__ float lse_mfma32(const float p[3], float k2, float sh, const uint4* __restrict__ At,
+                                            const float* __restrict__ Wt, int nrb, uint4* xa, uint4* xb, float* xs,
+                                            int lane) {
+#pragma clang fp contract(off)
+  {
+    unsigned x[3], y[3], z[3], P[3];
+    split3(p[0], x[0], x[1], x[2]);
+    split3(p[1], y[0], y[1], y[2]);
+    split3(p[2], z[0], z[1], z[2]);
+    split3(k2 * psq(p), P[0], P[1], P[2]);
+    xa[lane] = make_uint4(pack2(x[0], x[1]), pack2(x[2], y[0]), pack2(y[1], y[2]), pack2(z[0], z[1]));
+    xb[lane] = make_uint4(pack2(z[2], z[2]), pack2(P[0], P[1]), pack2(P[2], kBf16One), pack2(kBf16One, kBf16One));
+    if constexpr (FIXED) xs[lane] = sh;
+  }
+  __builtin_amdgcn_wave_barrier();
+  const int r = lane & 31, h = lane >> 5;
+#if RM_MFMA32 == 2
+  bf16x8 B0[2], B1[2];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    B0[cb] = __builtin_bit_cast(bf16x8, xa[32 * cb + r]);
+    B1[cb] = __builtin_bit_cast(bf16x8, h ? xb[32 * cb + r] : xa[32 * cb + r]);
+  }
+#endif
+  float S[2];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) S[cb] = FIXED ? xs[32 * cb + r] : 0.0f;
+  const float QMIN = k2 * 1e-6f;
+  float acc[2] = {0.0f, 0.0f};
+  if (nrb == 0) {
+    __builtin_amdgcn_wave_barrier();
+    return 0.0f;
+  }
+  const int n32 = nrb >> 1;  // nrb (16-sphere blocks) is even
+  const f32x16 zero = {};
+  const __amdgpu_buffer_rsrc_t ra = __builtin_amdgcn_make_buffer_rsrc((void*)At, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rw =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(Wt + (FIXED ? 32 : 0)), (short)0, 0x7fffffff, 0x00020000);
+  const int va = lane * 16, vw = h * 64;
+  auto load_a = [&](int rb, int m) {
+    if constexpr (BUF) return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(ra, va, (2 * rb + m) * 1024, 0));
+    else return __builtin_bit_cast(bf16x8, At[(2 * rb + m) * 64 + lane]);
+  };
+  auto load_w = [&](int rb, int i) {
+    if constexpr (BUF) return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw, vw + 16 * i, rb * 256, 0));
+    else return *reinterpret_cast<const float4*>(Wt + (FIXED ? 32 : 0) + rb * 64 + h * 16 + 4 * i);
+  };
+  auto consume = [&](const f32x16& D, const float4 (&w)[4], int cb) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float wv[4] = {w[i].x, w[i].y, w[i].z, w[i].w};
+      RM_M32_CONSUME_BODY
+    }
+  };
+  auto consume_ld = [&](const f32x16& D, int rb, int cb) {  // weights loaded as they are used
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float4 wi = load_w(rb, i);
+      const float wv[4] = {wi.x, wi.y, wi.z, wi.w};
+      RM_M32_CONSUME_BODY
+    }
+  };
+  bf16x8 A0 = load_a(0, 0), A1 = load_a(0, 1);
+  for (int rb = 0; rb < n32; ++rb) {
+    float4 w[4];
+#if RM_MFMA32 >= 2
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = load_w(rb, i);
+#endif
+#if RM_MFMA32 == 2  // both column blocks' tiles in flight (more registers)
+    f32x16 D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B0[0], zero, 0, 0, 0);
+    D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B1[0], D, 0, 0, 0);
+    f32x16 E = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B0[1], zero, 0, 0, 0);
+    E = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B1[1], E, 0, 0, 0);
+    const int rn = min(rb + 1, n32 - 1);
+    A0 = load_a(rn, 0);
+    A1 = load_a(rn, 1);
+    RM_SCHED_BARRIER();
+    consume(D, w, 0);
+    consume(E, w, 1);
+    RM_SCHED_BARRIER();
+#else  // one column block's tile at a time, the weights loaded as they are used (3: once per
+       // block of 32 spheres), the ray side re-read from the exchange (registers)
+    (void)w;
+    int z = 0;  // opaque 0: the ray-side reads stay in the loop (hoisted they hold 16 VGPRs)
+    asm volatile("" : "+s"(z));
+    const uint4* xah = xa + z;
+    const uint4* xbh = (h ? xb : xa) + z;
+    f32x16 D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, __builtin_bit_cast(bf16x8, xah[r]), zero, 0, 0, 0);
+    D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, __builtin_bit_cast(bf16x8, xbh[r]), D, 0, 0, 0);
+    RM_SCHED_BARRIER();
+#if RM_MFMA32 == 3  // the block's weights loaded once for both column blocks
+    consume(D, w, 0);
+#else
+    consume_ld(D, rb, 0);
+#endif
+    RM_SCHED_BARRIER();
+    D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, __builtin_bit_cast(bf16x8, xah[32 + r]), zero, 0, 0, 0);
+    D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, __builtin_bit_cast(bf16x8, xbh[32 + r]), D, 0, 0, 0);
+    const int rn = min(rb + 1, n32 - 1);
+    A0 = load_a(rn, 0);
+    A1 = load_a(rn, 1);
+    RM_SCHED_BARRIER();
+#if RM_MFMA32 == 3
+    consume(D, w, 1);
+#else
+    consume_ld(D, rb, 1);
+#endif
+    RM_SCHED_BARRIER();
+#endif
+  }
+  // lanes < 32 end with column block 0 (rays 0-31), lanes >= 32 with block 1: ray l either way
+  const float own = swap32_sum(acc[0], acc[1]);
+  __builtin_amdgcn_wave_barrier();
+  return own;
+}
+#endif
+
 // Split march (RM_MARCH_SPLIT): the kSplitWaves waves of a block hold the same 64 rays; wave w
 // sums the row blocks [part_rb(w), part_rb(w + 1)) (even bounds: lse_mfma runs pairs) and the
 // partial sums are added in wave order, so every wave gets the same total. comb: 64 floats per
@@ -817,7 +976,11 @@ __device__ __forceinline__ float march_d_none(const float p[3], float kappa, flo
                                               uint4* xa, uint4* xb, float* xs, int lane, float* comb = nullptr,
                                               int wave = 0) {
 #pragma clang fp contract(off)
+#if RM_MFMA32
+  float s = lse_mfma32<CLAMP, false, BUF>(p, kappa * kappa, 0.0f, At, Wt, nrb, xa, xb, xs, lane);
+#else
   float s = lse_mfma<CLAMP, false, BUF>(p, kappa * kappa, 0.0f, At, Wt, nrb, xa, xb, xs, lane);
+#endif
   if (comb != nullptr) s = split_combine(s, comb, wave, lane);
   return -flog2(fmaxf(s, 1e-30f)) * inv_kappa;
 }
@@ -841,7 +1004,11 @@ __device__ __forceinline__ float march_d_fixed(const float p[3], float kappa, fl
 #pragma clang fp contract(off)
   const float k2 = kappa * kappa;
   const float sh = fixed_shift(p, k2, S00, S10);
+#if RM_MFMA32
+  float s = lse_mfma32<CLAMP, true, BUF>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
+#else
   float s = lse_mfma<CLAMP, true, BUF>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
+#endif
   if (comb != nullptr) s = split_combine(s, comb, wave, lane);
   const float m = kr_first - sh;
   return -(flog2(fmaxf(s, 1e-30f)) + m) * inv_kappa;
