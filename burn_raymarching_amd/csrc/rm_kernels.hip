@@ -60,6 +60,9 @@
 #ifndef RM_MARCH_BUFLOAD
 #define RM_MARCH_BUFLOAD 1  // matrix-core fragments by buffer loads (0: global loads)
 #endif
+#ifndef RM_MARCH_PK
+#define RM_MARCH_PK 1  // lse_mfma accumulates with v_pk_fma_f32 (two chains per ray; 0: one fma chain)
+#endif
 #ifndef RM_MFMA32
 #define RM_MFMA32 0  // the march's matrix-core tiles as v_mfma_f32_32x32x16_bf16 (32 spheres x 32 rays)
 #endif
@@ -779,17 +782,32 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) D[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[cb], zero, 0, 0, 0);
   };
+#if RM_MARCH_PK  // packed accumulate: two chains per ray (v even / odd), one v_pk_fma_f32 per two terms
+  f2 acc2[4] = {sp(0.0f), sp(0.0f), sp(0.0f), sp(0.0f)};
+#endif
   auto consume = [&](const f32x4 (&D)[4], const float4& w) {
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
       float q[4] = {D[cb].x, D[cb].y, D[cb].z, D[cb].w};
       const float wv[4] = {w.x, w.y, w.z, w.w};
+#if RM_MARCH_PK
+      float e[4];
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        if constexpr (CLAMP) q[v] = qclamp(q[v], QMIN);
+        const float rho = fsqrt(q[v]);
+        e[v] = fexp2(FIXED ? S[cb] - rho : -rho);
+      }
+      acc2[cb] = fma2(f2{wv[0], wv[1]}, f2{e[0], e[1]}, acc2[cb]);
+      acc2[cb] = fma2(f2{wv[2], wv[3]}, f2{e[2], e[3]}, acc2[cb]);
+#else
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         if constexpr (CLAMP) q[v] = qclamp(q[v], QMIN);
         const float rho = fsqrt(q[v]);
         acc[cb] = fmaf(wv[v], fexp2(FIXED ? S[cb] - rho : -rho), acc[cb]);
       }
+#endif
     }
   };
   // one tile at a time (registers: the march must not spill at 128 VGPRs); the fragments of the
@@ -816,6 +834,10 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
   // v_permlane32_swap and one v_permlane16_swap, no LDS) leaves lane (n, g) with the total of
   // its own ray 16g + n: rows 0/2 keep the column blocks 0/2 summed over lane bit 5, rows 1/3
   // the blocks 1/3, then each row adds its bit-4 partner
+#if RM_MARCH_PK
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) acc[cb] = acc2[cb].x + acc2[cb].y;
+#endif
   const float own = swap16_sum(swap32_sum(acc[0], acc[2]), swap32_sum(acc[1], acc[3]));
   __builtin_amdgcn_wave_barrier();  // the exchange is rewritten by the next step
   return own;
