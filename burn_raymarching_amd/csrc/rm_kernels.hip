@@ -791,15 +791,18 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
       float q[4] = {D[cb].x, D[cb].y, D[cb].z, D[cb].w};
       const float wv[4] = {w.x, w.y, w.z, w.w};
 #if RM_MARCH_PK
-      float e[4];
+      float rho[4];
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
         if constexpr (CLAMP) q[v] = qclamp(q[v], QMIN);
-        const float rho = fsqrt(q[v]);
-        e[v] = fexp2(FIXED ? S[cb] - rho : -rho);
+        rho[v] = fsqrt(q[v]);
       }
-      acc2[cb] = fma2(f2{wv[0], wv[1]}, f2{e[0], e[1]}, acc2[cb]);
-      acc2[cb] = fma2(f2{wv[2], wv[3]}, f2{e[2], e[3]}, acc2[cb]);
+#pragma unroll
+      for (int v = 0; v < 4; v += 2) {
+        // FIXED: the shifted exponents two at a time (v_pk_add_f32: the same bits as two v_sub_f32)
+        const f2 x = FIXED ? sp(S[cb]) - f2{rho[v], rho[v + 1]} : f2{-rho[v], -rho[v + 1]};
+        acc2[cb] = fma2(f2{wv[v], wv[v + 1]}, f2{fexp2(x.x), fexp2(x.y)}, acc2[cb]);
+      }
 #else
 #pragma unroll
       for (int v = 0; v < 4; ++v) {
