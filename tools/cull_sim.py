@@ -52,13 +52,25 @@ def main():
     ap.add_argument("--steps", type=int, default=32)
     ap.add_argument("--k", type=float, default=32.0)
     ap.add_argument("--radius-range", type=float, nargs=2, default=(0.03, 0.12))
+    ap.add_argument("--scene-json", default="", help="a scene.json (e.g. the grown configs[4] model) instead "
+                                                     "of the synthetic ball; --spheres from the file")
+    ap.add_argument("--cameras", default="", help="cameras.json poses instead of the ring")
     args = ap.parse_args()
-    sc = rmm.synthetic_scene(args.spheres, seed=0, radius_range=tuple(args.radius_range))
-    c, r = sc["centers"].astype(float), sc["radius"].astype(float)
+    if args.scene_json:
+        from bench import load_scene_json
+        sc = load_scene_json(args.scene_json)
+        args.spheres = int(sc["centers"].shape[0])
+    else:
+        sc = rmm.synthetic_scene(args.spheres, seed=0, radius_range=tuple(args.radius_range))
+    c, r = np.asarray(sc["centers"], float), np.asarray(sc["radius"], float)
     orders = {"given": np.arange(len(c)), "morton": morton_order(c)}
     W = H = 512
     rng = np.random.default_rng(0)
-    cams = rmm.ring_cameras(10)
+    if args.cameras:
+        import json
+        cams = [(q["origin"], q["target"], q["fov"]) for q in json.load(open(args.cameras))]
+    else:
+        cams = rmm.ring_cameras(10)
     kl2 = args.k / math.log(2.0)  # base-2 exponent scale
     res = {name: [0, 0] for name in orders}
     # the conservative test a kernel can run: per row block a bounding sphere (c_b, R_b), per ray
