@@ -853,13 +853,8 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // of 16x16x32 per evaluation (each holds the SIMD's vector issue for 8 cycles). Lane (r, h) =
 // (l & 31, l >> 5) gets, per column block cb, 16 results of ray 32 cb + r: rows (i & 3) + 8 (i >> 2)
 // + 4 h (mfma_w_sphere's slot order); the two halves of a ray meet in one v_permlane32_swap.
-#define RM_M32_CONSUME_BODY                                          \
-  _Pragma("unroll") for (int v = 0; v < 4; ++v) {                     \
-    float q = D[4 * i + v];                                            \
-    if constexpr (CLAMP) q = qclamp(q, QMIN);                          \
-    const float rho = fsqrt(q);                                        \
-    acc[cb] = fmaf(wv[v], fexp2(FIXED ? S[cb] - rho : -rho), acc[cb]); \
-  }
+// Registers: one column block's tile at a time, the weights loaded as they are used, the ray side
+// re-read from the exchange (measured: Appendix A; 2 spilled VGPRs in the train kernel).
 template <bool CLAMP, bool FIXED, bool BUF = (RM_MARCH_BUFLOAD != 0)>
 __device__ __forceinline__ float lse_mfma32(const float p[3], float k2, float sh, const uint4* __restrict__ At,
                                             const float* __restrict__ Wt, int nrb, uint4* xa, uint4* xb, float* xs,
@@ -877,14 +872,6 @@ __device__ __forceinline__ float lse_mfma32(const float p[3], float k2, float sh
   }
   __builtin_amdgcn_wave_barrier();
   const int r = lane & 31, h = lane >> 5;
-#if RM_MFMA32 == 2
-  bf16x8 B0[2], B1[2];
-#pragma unroll
-  for (int cb = 0; cb < 2; ++cb) {
-    B0[cb] = __builtin_bit_cast(bf16x8, xa[32 * cb + r]);
-    B1[cb] = __builtin_bit_cast(bf16x8, h ? xb[32 * cb + r] : xa[32 * cb + r]);
-  }
-#endif
   float S[2];
 #pragma unroll
   for (int cb = 0; cb < 2; ++cb) S[cb] = FIXED ? xs[32 * cb + r] : 0.0f;
@@ -908,43 +895,22 @@ __device__ __forceinline__ float lse_mfma32(const float p[3], float k2, float sh
     if constexpr (BUF) return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw, vw + 16 * i, rb * 256, 0));
     else return *reinterpret_cast<const float4*>(Wt + (FIXED ? 32 : 0) + rb * 64 + h * 16 + 4 * i);
   };
-  auto consume = [&](const f32x16& D, const float4 (&w)[4], int cb) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float wv[4] = {w[i].x, w[i].y, w[i].z, w[i].w};
-      RM_M32_CONSUME_BODY
-    }
-  };
-  auto consume_ld = [&](const f32x16& D, int rb, int cb) {  // weights loaded as they are used
+  auto consume = [&](const f32x16& D, int rb, int cb) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const float4 wi = load_w(rb, i);
       const float wv[4] = {wi.x, wi.y, wi.z, wi.w};
-      RM_M32_CONSUME_BODY
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        float q = D[4 * i + v];
+        if constexpr (CLAMP) q = qclamp(q, QMIN);
+        const float rho = fsqrt(q);
+        acc[cb] = fmaf(wv[v], fexp2(FIXED ? S[cb] - rho : -rho), acc[cb]);
+      }
     }
   };
   bf16x8 A0 = load_a(0, 0), A1 = load_a(0, 1);
   for (int rb = 0; rb < n32; ++rb) {
-    float4 w[4];
-#if RM_MFMA32 >= 2
-#pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = load_w(rb, i);
-#endif
-#if RM_MFMA32 == 2  // both column blocks' tiles in flight (more registers)
-    f32x16 D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B0[0], zero, 0, 0, 0);
-    D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B1[0], D, 0, 0, 0);
-    f32x16 E = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, B0[1], zero, 0, 0, 0);
-    E = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, B1[1], E, 0, 0, 0);
-    const int rn = min(rb + 1, n32 - 1);
-    A0 = load_a(rn, 0);
-    A1 = load_a(rn, 1);
-    RM_SCHED_BARRIER();
-    consume(D, w, 0);
-    consume(E, w, 1);
-    RM_SCHED_BARRIER();
-#else  // one column block's tile at a time, the weights loaded as they are used (3: once per
-       // block of 32 spheres), the ray side re-read from the exchange (registers)
-    (void)w;
     int z = 0;  // opaque 0: the ray-side reads stay in the loop (hoisted they hold 16 VGPRs)
     asm volatile("" : "+s"(z));
     const uint4* xah = xa + z;
@@ -952,11 +918,7 @@ __device__ __forceinline__ float lse_mfma32(const float p[3], float k2, float sh
     f32x16 D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, __builtin_bit_cast(bf16x8, xah[r]), zero, 0, 0, 0);
     D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, __builtin_bit_cast(bf16x8, xbh[r]), D, 0, 0, 0);
     RM_SCHED_BARRIER();
-#if RM_MFMA32 == 3  // the block's weights loaded once for both column blocks
-    consume(D, w, 0);
-#else
-    consume_ld(D, rb, 0);
-#endif
+    consume(D, rb, 0);
     RM_SCHED_BARRIER();
     D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A0, __builtin_bit_cast(bf16x8, xah[32 + r]), zero, 0, 0, 0);
     D = __builtin_amdgcn_mfma_f32_32x32x16_bf16(A1, __builtin_bit_cast(bf16x8, xbh[32 + r]), D, 0, 0, 0);
@@ -964,13 +926,8 @@ __device__ __forceinline__ float lse_mfma32(const float p[3], float k2, float sh
     A0 = load_a(rn, 0);
     A1 = load_a(rn, 1);
     RM_SCHED_BARRIER();
-#if RM_MFMA32 == 3
-    consume(D, w, 1);
-#else
-    consume_ld(D, rb, 1);
-#endif
+    consume(D, rb, 1);
     RM_SCHED_BARRIER();
-#endif
   }
   // lanes < 32 end with column block 0 (rays 0-31), lanes >= 32 with block 1: ray l either way
   const float own = swap32_sum(acc[0], acc[1]);
