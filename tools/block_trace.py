@@ -128,9 +128,12 @@ def analyse(tr, bins=40, steps=0):
               f"live mean {run_steps[live].mean() if live.any() else 0:.1f}")
         # where the waves' time goes, summed over all waves (wall time of each wave, so a phase's
         # share includes its SIMD sharing: a proxy for its share of the launch's issue)
-        m_all = np.clip(np.where(live, tm, e) - s, 0, None)
-        p_all = np.where(live, tp - tm, 0.0)
-        b_all = np.where(live, e - tp, 0.0)
+        # (stamps outside the wave's own [start, end] are stale: a wave that ended before writing
+        # them, e.g. an empty block of a continuation launch, counts as march time only)
+        ok = live & (tm >= s) & (tp >= tm) & (e >= tp)
+        m_all = np.where(ok, tm - s, e - s)
+        p_all = np.where(ok, tp - tm, 0.0)
+        b_all = np.where(ok, e - tp, 0.0)
         tot = m_all.sum() + p_all.sum() + b_all.sum()
         print(f"summed wave time: march {m_all.sum() / tot:.3f}, post-march forward {p_all.sum() / tot:.3f}, "
               f"backward {b_all.sum() / tot:.3f} (of {tot / 1e3:.1f} wave-ms)")
