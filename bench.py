@@ -322,6 +322,11 @@ def main():
         ring = max(args.ring, shard.views_total)
         cams = [rmm.ring_cameras(ring)[a] for a in ring_order(ring, args.ring_order)]
     shard.ring = ring
+    if use_graph and shard.views_total != ring:
+        # a captured step freezes its views, target slice and camera bases: replays would train the
+        # captured views while eager steps rotate through the ring -- not the same run
+        raise SystemExit(f"--graph on needs the same views every step: {shard.views_total} views per step "
+                         f"on a ring of {ring} rotate (use --ring {shard.views_total})")
     targets = torch.empty((ring, npix, 3), device="cuda")
     if args.targets == "files":
         targets.copy_(torch.from_numpy(load_target_files(args.cameras, cam_entries, W, H)).view(ring, npix, 3))

@@ -8,7 +8,9 @@ Run ``python -m burn_raymarching_amd._build`` or ``__graft_entry__.build()``.
 """
 from __future__ import annotations
 
+import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -36,13 +38,41 @@ def _stale(target: str, sources) -> bool:
     return any(os.path.getmtime(s) > t for s in sources)
 
 
+# The kernel library's sources; their hash is compiled into rm_version() ("src <hash>"), so that a
+# shipped .so names the source it came from (tests/test_abi.py compares it with the tree).
+KERNEL_SOURCES = [os.path.join(CSRC, "rm_kernels.hip"), os.path.join(CSRC, "rm_device.h"),
+                  os.path.join(CSRC, "rm_small.h"), os.path.join(ROOT, "include", "raymarch.h")]
+
+
+def source_hash(paths=None) -> str:
+    """sha256 (first 16 hex digits) over the kernel sources' names and bytes, in order."""
+    h = hashlib.sha256()
+    for p in paths or KERNEL_SOURCES:
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+        h.update(b"\0")
+    return h.hexdigest()[:16]
+
+
+def lib_source_hash(path: str = LIB):
+    """The source hash compiled into a built kernel library (read from the file, not loaded)."""
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        m = re.search(rb"\(gfx950\) src ([0-9a-f]{16})", f.read())
+    return m.group(1).decode() if m else None
+
+
 def build_lib(force: bool = False, verbose: bool = False) -> str:
     os.makedirs(LIBDIR, exist_ok=True)
-    srcs = [os.path.join(CSRC, "rm_kernels.hip"), os.path.join(CSRC, "rm_device.h"), os.path.join(CSRC, "rm_small.h"),
-            os.path.join(ROOT, "include", "raymarch.h")]
-    if force or _stale(LIB, srcs):
+    srcs = KERNEL_SOURCES
+    sha = source_hash(srcs)
+    # rebuilt when the embedded hash differs from the tree's (mtimes alone miss a checkout of
+    # older sources), or when a source is newer than the library
+    if force or _stale(LIB, srcs) or lib_source_hash(LIB) != sha:
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-Wall", "-Wno-unused-result", "-o", LIB, srcs[0]]
+               "-Wall", "-Wno-unused-result", f'-DRM_SOURCE_SHA="{sha}"', "-o", LIB, srcs[0]]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)

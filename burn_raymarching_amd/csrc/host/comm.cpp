@@ -11,7 +11,8 @@
 // Rendezvous (rmh_rendezvous_*): rank 0 creates the ncclUniqueId and publishes it in a file
 // (written to a temporary name and renamed, so readers never see a partial id) tagged with the
 // run's id; the other ranks poll for a complete file with the same run id. No clock is involved:
-// a rank may start, or finish its HIP initialisation, any time before the timeout.
+// a rank may start, or finish its HIP initialisation, any time before the timeout. The id must
+// name the run (not empty, not torchrun's default "none"), or a stale file could pass for it.
 //
 // Watchdog (rmh_collective.wait): a peer that died mid-run leaves the others spinning inside an
 // RCCL kernel on their stream (over xGMI nothing reports the loss). The driver waits on its stream
@@ -109,6 +110,19 @@ std::string resolve_run_id(const char* run_id) {
   return std::string();
 }
 
+// A run id that names this run: not empty, and not torchrun's default "none" (every run launched
+// without --rdzv-id has it). With such an id a file a crashed earlier run left at the same path
+// would pass for this run's, and a rank that polls before rank 0 replaces it would join a dead
+// ncclUniqueId (ncclCommInitRank has no timeout): the rendezvous refuses it.
+int check_run_id(const std::string& id) {
+  if (id.empty() || id == "none")
+    return fail(RMH_ERR_INVALID_ARG,
+                "the id-file rendezvous needs a run id naming this run (run_id, env RMH_RUN_ID or "
+                "TORCHELASTIC_RUN_ID; got '%s'): a stale file of an earlier run could pass for this run's",
+                id.c_str());
+  return RMH_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -116,6 +130,7 @@ extern "C" {
 int rmh_rendezvous_publish(const char* path, const char* run_id, const void* blob, int64_t size) {
   if (!path || !blob || size < 0 || size > (1 << 20)) return fail(RMH_ERR_INVALID_ARG, "bad rendezvous arguments");
   const std::string id = resolve_run_id(run_id);
+  if (const int rc = check_run_id(id)) return rc;
   std::string data(kMagic, sizeof kMagic);
   const uint32_t n = (uint32_t)id.size();
   const uint64_t sz = (uint64_t)size;
@@ -131,6 +146,7 @@ int rmh_rendezvous_publish(const char* path, const char* run_id, const void* blo
 int rmh_rendezvous_read(const char* path, const char* run_id, void* blob, int64_t size, double timeout_s) {
   if (!path || !blob || size < 0) return fail(RMH_ERR_INVALID_ARG, "bad rendezvous arguments");
   const std::string id = resolve_run_id(run_id);
+  if (const int rc = check_run_id(id)) return rc;
   const auto t0 = std::chrono::steady_clock::now();
   std::string seen;  // why the last file present was not taken (for the timeout message)
   for (;;) {
@@ -170,6 +186,12 @@ int rmh_collective_rccl_create(int32_t rank, int32_t world, int32_t device, cons
   if (!out || world < 1 || rank < 0 || rank >= world || (world > 1 && !id_path) || !(timeout_s > 0.0))
     return fail(RMH_ERR_INVALID_ARG, "bad collective arguments (rank %d, world %d)", rank, world);
   std::memset(out, 0, sizeof *out);
+  if (world > 1) {  // before any GPU call: a launch without a run id fails at once
+    if (const int rc = check_run_id(resolve_run_id(run_id))) {
+      const std::string why = rmh_last_error();
+      return fail(rc, "rank %d: %s", rank, why.c_str());
+    }
+  }
   if (hipSetDevice(device) != hipSuccess) return fail(RMH_ERR_GPU, "hipSetDevice(%d) failed", device);
   ncclUniqueId id;
   ncclResult_t r;

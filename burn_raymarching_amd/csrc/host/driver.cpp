@@ -74,6 +74,9 @@ struct Gpu {
   }
 };
 
+// Training steps a rank enqueues ahead of the GPU when it runs with collectives (rmh_train).
+constexpr int32_t kStepsInFlight = 32;
+
 // Waits for the driver's stream: through the collective's watchdog when collectives may be in
 // flight (a dead peer then ends in an error instead of a hang), else hipStreamSynchronize.
 int sync_stream(const Gpu& g, const rmh_collective* comm) {
@@ -201,9 +204,13 @@ void rmh_train_config_default(rmh_train_config* c) {
 int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_out, int32_t raw_capacity) {
   if (!cfg || !cfg->cameras_json) return fail(RMH_ERR_INVALID_ARG, "NULL config");
   if (cfg->width < 1 || cfg->height < 1 || cfg->stages < 1 || cfg->steps_per_stage < 1 || cfg->batch < 1 ||
-      cfg->march_steps < 1 || !(cfg->split_scale >= 0.0f) || !(cfg->split_move >= 0.0f) || cfg->max_spheres < 0)
+      cfg->march_steps < 1 || std::isnan(cfg->split_scale) || std::isnan(cfg->split_move) || cfg->max_spheres < 0)
     return fail(RMH_ERR_INVALID_ARG, "bad training configuration");
   const bool f16 = cfg->color_f16 != 0;
+  // the growth knobs: 0 (a zeroed struct) = the reference's value, < 0 = no such condition
+  // (rmh_prune_and_split_ex takes 0 for that) -- ADVICE r04: a zeroed config is the reference rule
+  const float split_scale = cfg->split_scale == 0.0f ? 1.0f : std::max(cfg->split_scale, 0.0f);
+  const float split_move = cfg->split_move == 0.0f ? 0.05f : std::max(cfg->split_move, 0.0f);
   const int32_t W = cfg->width, H = cfg->height;
   const rmh_collective* comm = cfg->comm;
   const int32_t world = comm ? comm->world : 1, rank = comm ? comm->rank : 0;
@@ -371,6 +378,13 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
                                          cfg->weight_decay, 1, read_loss ? d_loss + 1 : nullptr, d_act.f()));
       }
       ++steps_done;
+      // With collectives every rank drains its stream under the watchdog every kStepsInFlight
+      // steps, not only where rank 0 reads the loss: a rank whose peer stopped then meets the
+      // watchdog within kStepsInFlight steps instead of blocking inside a launch or ncclAllReduce
+      // once the HIP queue fills, and the watchdog's timeout measures at most that many steps of
+      // queued work, not a whole stage's backlog.
+      if (comm && world > 1 && !read_loss && step % kStepsInFlight == 0 && (rc = sync_stream(g, comm)) != RMH_OK)
+        return rc;
       if (read_loss) {
         float s[2];
         // drain the stream under the watchdog first: a copy to pageable memory blocks unguarded
@@ -408,8 +422,8 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
     int32_t nextM = 0;
     int split_rc = RMH_OK;
     if (lead)
-      split_rc = rmh_prune_and_split_ex(raw.data(), M, init_centers.data(), stage, cfg->stages, cfg->split_scale,
-                                        cfg->split_move, cfg->max_spheres, &rng_split, next.data(), &nextM);
+      split_rc = rmh_prune_and_split_ex(raw.data(), M, init_centers.data(), stage, cfg->stages, split_scale,
+                                        split_move, cfg->max_spheres, &rng_split, next.data(), &nextM);
     if (split_rc != RMH_OK && !comm) return split_rc;
     if (comm) {  // (with one rank too: the RCCL path is the same)
       DevBuf d_next;

@@ -4,14 +4,16 @@
 //   rm_train train    [--cameras data/cameras.json] [--out .] [--stages 5] [--steps 700]
 //                     [--batch 16384] [--size 256x256] [--march-steps 40] [--seed 0]
 //                     [--log-every 100] [--no-previews] [--device 0] [--ranks N]
-//                     [--split-scale 1] [--split-move 0.05] [--max-spheres 0] [--color-f16]
+//                     [--split-scale 1] [--split-move 0.05] [--split-all] [--max-spheres 0]
+//                     [--color-f16]
 //     --ranks N: data-parallel training on N GPUs (devices 0..N-1), one process per GPU over
 //     RCCL: this process forks the N rank processes before anything touches a GPU and waits
 //     for them. (--rank r --world N --comm-file F [--run-id S] [--comm-timeout SEC] run one rank
 //     of a run launched elsewhere: every rank of the run gets the same F and S.)
-//     --split-scale / --split-move: prune_and_split's split thresholds (rmh_prune_and_split_ex;
-//     0 and 0 split every surviving sphere, for growth runs such as BASELINE configs[4];
-//     --max-spheres caps the next generation, 0 = no cap);
+//     --split-scale / --split-move: prune_and_split's split threshold scale and minimum move
+//     (rmh_train_config: 0 = the reference's 1 / 0.05, negative = no such condition);
+//     --split-all: every surviving sphere splits (both negative: growth runs such as BASELINE
+//     configs[4]); --max-spheres caps the next generation, 0 = no cap;
 //     --color-f16: fp16 colour / fp32 SDF.
 //   rm_train generate [--out data] [--prefix data/] [--size 256x256] [--device 0]
 //   rm_train preview  --scene scene.json --png out.png [--size 256x256]
@@ -35,7 +37,7 @@ int usage() {
                "usage: rm_train train|generate|preview [options]\n"
                "  train    --cameras F --out D --stages N --steps N --batch N --size WxH --march-steps N\n"
                "           --seed N --log-every N --no-previews --device N --ranks N\n"
-               "           --split-scale F --split-move F --max-spheres N --color-f16\n"
+               "           --split-scale F --split-move F --split-all --max-spheres N --color-f16\n"
                "           --rank R --world N --comm-file F --run-id S --comm-timeout SEC\n"
                "  generate --out D --prefix P --size WxH --device N\n"
                "  preview  --scene F --png F --size WxH --eye x,y,z --target x,y,z --fov F --radius-offset F\n");
@@ -137,6 +139,9 @@ int main(int argc, char** argv) {
       const std::string a = argv[i];
       if (a == "--no-previews") {
         cfg.previews = 0;
+      } else if (a == "--split-all") {  // every surviving sphere splits (configs[4] growth runs)
+        cfg.split_scale = -1.0f;
+        cfg.split_move = -1.0f;
       } else if (a == "--color-f16") {
         cfg.color_f16 = 1;
       } else if (!need(i)) {

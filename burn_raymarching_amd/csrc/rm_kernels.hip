@@ -93,9 +93,6 @@ static_assert(RM_ORDER_CNT_STRIDE >= RM_ORDER_CLASSES * RM_ORDER_CLS_STRIDE && R
 #ifndef RM_RED_ARR_STRIDE
 #define RM_RED_ARR_STRIDE 32  // unsigneds between rm_reduce_partials' arrival counters: a 128-byte line each
 #endif
-#ifndef RM_BWD_COMB_BUFS
-#define RM_BWD_COMB_BUFS 1  // transposed backward: combine buffers (1 keeps the block's LDS <= 32 KB)
-#endif
 
 namespace rm {
 
@@ -126,8 +123,19 @@ constexpr long long kSplitMaxRaysWide = 1048576;
 #ifndef RM_CONT_MIN_WAVES
 #define RM_CONT_MIN_WAVES RM_SPLIT_MIN_WAVES  // register budget of the split continuation kernel
 #endif
-constexpr int kSplitWaves = RM_SPLIT_WAVES;  // waves per 64-ray block of the split march (2 or 4)
+constexpr int kSplitWaves = RM_SPLIT_WAVES;  // waves per ray group of the split march (2 or 4)
 static_assert(kSplitWaves == 2 || kSplitWaves == 4, "split blocks have 2 or 4 waves");
+#ifndef RM_SPLIT_RAYS
+#define RM_SPLIT_RAYS 64
+#endif
+// Rays per split block (64, 32 or 16). Below 64 every wave of the block holds each of its rays
+// 64 / kSplitRays times (lane l and l + kSplitRays carry the same ray, bit for bit) and the
+// march's matrix-core tiles run kSplitRays / 16 column blocks instead of 4: a march step of a
+// block costs its waves kSplitRays / 64 of the 64-ray step, so heavy rays hold their SIMDs for
+// shorter and the blocks that march to the end are smaller work units (configs[4]).
+constexpr int kSplitRays = RM_SPLIT_RAYS;
+static_assert(kSplitRays == 64 || kSplitRays == 32 || kSplitRays == 16, "split blocks hold 64, 32 or 16 rays");
+constexpr int kSplitCB = kSplitRays / 16;  // column blocks of 16 rays in the split march's tiles
 constexpr long long kSplitMaxRays = 262144;
 #ifndef RM_REDUCE_SEGS
 #define RM_REDUCE_SEGS 128
@@ -300,12 +308,12 @@ struct Lds {  // the sphere records (global, scalar-loaded) plus the kernel's LD
 
 // LDS: the backward's two partial buffers, or (during the march) lse_mfma's per-wave ray
 // exchange (64 x (16 + 16 + 4) B per wave); then 256 B of misc scratch.
-// The transposed backward (RM_BWD_TRANSPOSED) uses RM_BWD_COMB_BUFS x kWaves x 8 x 64 combine
-// floats, 15 x 64 ray-data floats (field-major) and 64 g_t floats per wave. The LDS of a block decides how
-// many blocks a CU holds once waves leave the march early (their registers free up, the block's
-// LDS stays until its last wave ends): 24.3 KB -> 6 blocks per CU, 32.3 KB -> 4.
-constexpr size_t kSlotBwdT =
-    ((size_t)RM_BWD_COMB_BUFS * kWaves * 8 * 64 + (size_t)kWaves * 64 * 16) * sizeof(float);
+// The transposed backward (RM_BWD_TRANSPOSED) uses 15 x 64 ray-data floats (field-major) per wave
+// and kWaves x 64 g_t shares per wave (19.3 KB). The LDS of a block decides how many blocks a CU
+// holds once waves leave the march early (their registers free up, the block's LDS stays until its
+// last wave ends): 19.3 KB -> 8 blocks per CU (24.3 KB -> 6, 32.3 KB -> 4).
+constexpr int kBwdFields = 15;  // ray-image fields of the transposed backward
+constexpr size_t kSlotBwdT = ((size_t)kWaves * 64 * kBwdFields + (size_t)kWaves * kWaves * 64) * sizeof(float);
 constexpr size_t kSlotBytes0 = (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float) > (size_t)kWaves * 64 * 36
                                    ? (size_t)2 * kWaves * kChunkBwd * 8 * sizeof(float)
                                    : (size_t)kWaves * 64 * 36;
@@ -728,13 +736,18 @@ __device__ __forceinline__ void lse_point(const float p[3], const Lds& L, int np
 // (FIXED; w = 2^(k (r - r_0)), sh = the ray's own shift) for the lane's own ray -- the same sum
 // as lse_weighted up to fp32 rounding. xa / xb / xs: this wave's LDS exchange (64 uint4, 64
 // uint4, 64 floats).
-template <bool CLAMP, bool FIXED, bool BUF = (RM_MARCH_BUFLOAD != 0)>
+// NCB < 4 (the split march's smaller ray groups, kSplitRays): the wave's lanes hold 16 NCB rays,
+// lane l the ray of lane l mod 16 NCB; only the first NCB column blocks are multiplied and summed,
+// and the reduction takes the missing blocks as copies of the present ones. A ray's sum is the
+// same chain of the same terms as with NCB = 4 (the same bits; IEEE addition is commutative).
+template <bool CLAMP, bool FIXED, bool BUF = (RM_MARCH_BUFLOAD != 0), int NCB = 4>
 __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, const uint4* __restrict__ At,
                                           const float* __restrict__ Wt, int nrb, uint4* xa, uint4* xb, float* xs,
                                           int lane) {
   // no fp contraction: the record kernel's origin step (write_origins) runs this code in another
   // kernel and must reproduce it bit for bit
 #pragma clang fp contract(off)
+  static_assert(NCB == 1 || NCB == 2 || NCB == 4, "column blocks per wave");
   {  // the lane's own ray: Sa, Sb and the shift into the exchange
     unsigned x[3], y[3], z[3], P[3];
     split3(p[0], x[0], x[1], x[2]);
@@ -748,10 +761,10 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
   __builtin_amdgcn_wave_barrier();
   const int n = lane & 15, g = lane >> 4;
   const uint4* src = g < 3 ? xa : xb;
-  bf16x8 B[4];
-  float S[4];
+  bf16x8 B[NCB];
+  float S[NCB];
 #pragma unroll
-  for (int cb = 0; cb < 4; ++cb) {
+  for (int cb = 0; cb < NCB; ++cb) {
     B[cb] = __builtin_bit_cast(bf16x8, src[16 * cb + n]);
     S[cb] = FIXED ? xs[16 * cb + n] : 0.0f;
   }
@@ -778,16 +791,18 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
     if constexpr (BUF) return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rw, vw, rb * 128, 0));
     else return *reinterpret_cast<const float4*>(wsrc + rb * 32);
   };
-  auto tile = [&](const bf16x8& A, f32x4 (&D)[4]) {
+  auto tile = [&](const bf16x8& A, f32x4 (&D)[NCB]) {
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) D[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[cb], zero, 0, 0, 0);
+    for (int cb = 0; cb < NCB; ++cb) D[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(A, B[cb], zero, 0, 0, 0);
   };
 #if RM_MARCH_PK  // packed accumulate: two chains per ray (v even / odd), one v_pk_fma_f32 per two terms
-  f2 acc2[4] = {sp(0.0f), sp(0.0f), sp(0.0f), sp(0.0f)};
-#endif
-  auto consume = [&](const f32x4 (&D)[4], const float4& w) {
+  f2 acc2[NCB];
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
+  for (int cb = 0; cb < NCB; ++cb) acc2[cb] = sp(0.0f);
+#endif
+  auto consume = [&](const f32x4 (&D)[NCB], const float4& w) {
+#pragma unroll
+    for (int cb = 0; cb < NCB; ++cb) {
       float q[4] = {D[cb].x, D[cb].y, D[cb].z, D[cb].w};
       const float wv[4] = {w.x, w.y, w.z, w.w};
 #if RM_MARCH_PK
@@ -815,7 +830,7 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
   };
   // one tile at a time (registers: the march must not spill at 128 VGPRs); the fragments of the
   // next row block load while the lanes work on this one (nrb is even: Mpad % 32 == 0)
-  f32x4 D[4];
+  f32x4 D[NCB];
   bf16x8 A = load_a(0);
   float4 w = load_w(0);
   for (int rb = 0; rb < nrb; rb += 2) {
@@ -839,8 +854,11 @@ __device__ __forceinline__ float lse_mfma(const float p[3], float k2, float sh, 
   // the blocks 1/3, then each row adds its bit-4 partner
 #if RM_MARCH_PK
 #pragma unroll
-  for (int cb = 0; cb < 4; ++cb) acc[cb] = acc2[cb].x + acc2[cb].y;
+  for (int cb = 0; cb < NCB; ++cb) acc[cb] = acc2[cb].x + acc2[cb].y;
 #endif
+  // NCB < 4: column block cb + NCB is a copy of block cb (the lanes' rays repeat every 16 NCB)
+#pragma unroll
+  for (int cb = NCB; cb < 4; ++cb) acc[cb] = acc[cb - NCB];
   const float own = swap16_sum(swap32_sum(acc[0], acc[2]), swap32_sum(acc[1], acc[3]));
   __builtin_amdgcn_wave_barrier();  // the exchange is rewritten by the next step
   return own;
@@ -952,7 +970,7 @@ __device__ __forceinline__ float split_combine(float part, float* comb, int wave
 // A march step's soft-min D at p on the matrix cores without a shift (soft_min_march's
 // unshifted step; shared with write_origins like march_d_fixed). comb != nullptr: a split
 // block's wave, At / Wt / nrb its quarter (split_combine).
-template <bool CLAMP, bool BUF = (RM_MARCH_BUFLOAD != 0)>
+template <bool CLAMP, bool BUF = (RM_MARCH_BUFLOAD != 0), int NCB = 4>
 __device__ __forceinline__ float march_d_none(const float p[3], float kappa, float inv_kappa,
                                               const uint4* __restrict__ At, const float* __restrict__ Wt, int nrb,
                                               uint4* xa, uint4* xb, float* xs, int lane, float* comb = nullptr,
@@ -961,7 +979,7 @@ __device__ __forceinline__ float march_d_none(const float p[3], float kappa, flo
 #if RM_MFMA32
   float s = lse_mfma32<CLAMP, false, BUF>(p, kappa * kappa, 0.0f, At, Wt, nrb, xa, xb, xs, lane);
 #else
-  float s = lse_mfma<CLAMP, false, BUF>(p, kappa * kappa, 0.0f, At, Wt, nrb, xa, xb, xs, lane);
+  float s = lse_mfma<CLAMP, false, BUF, NCB>(p, kappa * kappa, 0.0f, At, Wt, nrb, xa, xb, xs, lane);
 #endif
   if (comb != nullptr) s = split_combine(s, comb, wave, lane);
   return -flog2(fmaxf(s, 1e-30f)) * inv_kappa;
@@ -978,7 +996,7 @@ __device__ __forceinline__ float fixed_shift(const float p[3], float k2, const f
 // A march step's soft-min D at p on the matrix cores with the fixed shift sh = rho'_0 (sphere 0;
 // S00 / S10 = its records S0[0] / S1[0]) -- soft_min_march's fixed-shift step, shared with the
 // per-view origin step (write_origins) so that both give the same bits.
-template <bool CLAMP, bool BUF = (RM_MARCH_BUFLOAD != 0)>
+template <bool CLAMP, bool BUF = (RM_MARCH_BUFLOAD != 0), int NCB = 4>
 __device__ __forceinline__ float march_d_fixed(const float p[3], float kappa, float inv_kappa, float kr_first,
                                                const float4& S00, const float4& S10, const uint4* __restrict__ At,
                                                const float* __restrict__ Wt, int nrb, uint4* xa, uint4* xb,
@@ -989,7 +1007,7 @@ __device__ __forceinline__ float march_d_fixed(const float p[3], float kappa, fl
 #if RM_MFMA32
   float s = lse_mfma32<CLAMP, true, BUF>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
 #else
-  float s = lse_mfma<CLAMP, true, BUF>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
+  float s = lse_mfma<CLAMP, true, BUF, NCB>(p, k2, sh, At, Wt, nrb, xa, xb, xs, lane);
 #endif
   if (comb != nullptr) s = split_combine(s, comb, wave, lane);
   const float m = kr_first - sh;
@@ -1560,7 +1578,8 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   } else {
     blk = ray_block(a, &cls);
   }
-  const long long li = SPLIT ? blk * 64 + lane : blk * kBlock + tid;
+  // SPLIT: lane l holds ray l mod kSplitRays of the group (kSplitRays < 64: copies, see kSplitRays)
+  const long long li = SPLIT ? blk * kSplitRays + (lane & (kSplitRays - 1)) : blk * kBlock + tid;
 #if RM_HEAVY_PRIO
   // the dearest class's waves first at the SIMD's issue arbiter: they set the launch's critical
   // path, the cheaper waves fill the issue slots they leave
@@ -1569,9 +1588,10 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   const bool valid = li < a.n_rays;
   long long ri = a.ray_begin + (valid ? li : 0);  // becomes the ray's row in the [N,3] tensors
   // the wave that writes this ray's outputs; SPLIT: all four waves run the post-march forward
-  // (each over a quarter of the spheres, merged) and wave w seeds the backward of lanes 16w..16w+15
-  const bool own_rays = !SPLIT || wave == 0;
-  const bool seed_lane = !SPLIT || (lane >> 4) == wave;
+  // (each over a quarter of the spheres, merged) and wave w seeds the backward of the group's rays
+  // [w R / 4, (w + 1) R / 4) (R = kSplitRays; lanes past R carry copies and seed nothing)
+  const bool own_rays = !SPLIT || (wave == 0 && lane < kSplitRays);
+  const bool seed_lane = !SPLIT || (wave == 0 && lane < kSplitRays);
 
   const float kappa = a.k * kLog2e, nkappa = -kappa, inv_kappa = 1.0f / kappa;
 
@@ -1722,13 +1742,14 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
         Wt += (size_t)r0 * 32;
         comb = L.slots + kSplitCombOff + (split_par ^= 1) * (kWaves * 64);
       }
+      constexpr int kNcb = SPLIT ? kSplitCB : 4;  // column blocks of this wave's rays
       if (fixed) {  // the ray's shift: rho'_0 of sphere 0 (any value near it keeps +-100 headroom)
         const float4 A = Lds::v4(L.S0[0]), B = Lds::v4(L.S1[0]);
-        Dm = fast ? march_d_fixed<false, kBuf>(p, kappa, inv_kappa, kr_first, A, B, At, Wt, nq, xa, xb, xs, lane, comb, wave)
-                  : march_d_fixed<true, kBuf>(p, kappa, inv_kappa, kr_first, A, B, At, Wt, nq, xa, xb, xs, lane, comb, wave);
+        Dm = fast ? march_d_fixed<false, kBuf, kNcb>(p, kappa, inv_kappa, kr_first, A, B, At, Wt, nq, xa, xb, xs, lane, comb, wave)
+                  : march_d_fixed<true, kBuf, kNcb>(p, kappa, inv_kappa, kr_first, A, B, At, Wt, nq, xa, xb, xs, lane, comb, wave);
       } else {
-        Dm = fast ? march_d_none<false, kBuf>(p, kappa, inv_kappa, At, Wt, nq, xa, xb, xs, lane, comb, wave)
-                  : march_d_none<true, kBuf>(p, kappa, inv_kappa, At, Wt, nq, xa, xb, xs, lane, comb, wave);
+        Dm = fast ? march_d_none<false, kBuf, kNcb>(p, kappa, inv_kappa, At, Wt, nq, xa, xb, xs, lane, comb, wave)
+                  : march_d_none<true, kBuf, kNcb>(p, kappa, inv_kappa, At, Wt, nq, xa, xb, xs, lane, comb, wave);
       }
       (void)k2;
 #ifdef RM_BLOCK_TRACE
@@ -1879,7 +1900,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     }
     for (int st = st0; !dead && st < a.steps; ++st) {
       if (SPLIT && a.cont_cap > 0 && st == a.cont_cap) {  // defer: save the state at the top of this step
-        if (wave == 0) {  // the four waves hold the same state
+        if (wave == 0 && lane < kSplitRays) {  // the four waves (and a ray's copies) hold the same state
           float* cs = a.cont_state;
           const long long R = a.cont_rays;
           cs[li] = t;
@@ -2240,55 +2261,124 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   };
 
 #if RM_BWD_TRANSPOSED
-  // ---- backward sweeps with one sphere per lane (transposed). The per-sphere gradient sums
-  // over the wave's rays accumulate in each lane's registers (no cross-lane reduction); the
-  // rays are visited one pair per packed instruction, their data broadcast from LDS. Only the
-  // position gradient g_p of sweep 1 is a per-ray sum over spheres, and only g_t = g_p . d
-  // (the ray direction) is needed (t_final = t + D(p_a), p = o + d t_final): that scalar is
-  // reduced across the lanes for batches of 8 rays (one transposing reduction) and accumulated
-  // in LDS over the sphere groups. Rays whose seeds are zero contribute exact zeros and are skipped (sweep 1:
-  // gm = 0 and b_scale = 0; sweep 2: g_t = 0) -- in practice the escaped rays of live waves:
-  // the others are compacted (rank among the active lanes) into a field-major per-wave LDS
-  // image, so that rays 2i and 2i+1 of the list sit side by side in every field and one
-  // ds_read_b64 per field yields a packed pair (no register moves, wave-uniform addresses). An
-  // odd count is padded with a copy of the last ray whose seeds are zero (exact zero terms).
-  // Distances are formed with the same fp32 operations and operands as the forward sweeps
-  // (qpair, delta_pair_rsq), so dd = dmin - delta <= 0 and v - mA <= 0 hold exactly, as in the
-  // lane=ray form.
+  // ---- backward sweeps with one sphere per lane (transposed), the work shared out over the
+  // block's live waves. Each live wave publishes its rays with non-zero seeds (a source) as a
+  // compacted field-major LDS image. The work units are (64-sphere group, source wave) pairs in
+  // group-major order; live wave r of n takes the units [r U / n, (r + 1) U / n) (U = groups x
+  // sources). For each sphere of its lane a wave sums the terms of the rays of its units (sources
+  // in wave order, their rays two per packed instruction) in registers, and writes the group's
+  // record columns itself when it holds every source of the group; a group whose sources span
+  // waves is added up from the waves' partials in LDS, in source order, by the wave that holds its
+  // first unit. So each sphere group is loaded by one wave (two at a split), and there is no
+  // combine of wave partials and no barrier per group. A split block's waves hold the same rays:
+  // wave 0 is its one source (it seeds every lane) and the waves share the groups.
+  // Only the position gradient g_p of sweep 1 is a per-ray sum over spheres, and only g_t = g_p . d
+  // (the ray direction) is needed (t_final = t + D(p_a), p = o + d t_final): each computing wave
+  // reduces its share across the lanes for batches of 8 rays (one transposing reduction) into an
+  // LDS slot per (computing wave, source wave, ray), and the ray's owner adds the computing waves'
+  // shares in wave order. Rays whose seeds are zero contribute exact zeros and are not listed
+  // (sweep 1: gm = 0 and b_scale = 0; sweep 2: g_t = 0) -- in practice the escaped rays of live
+  // waves; an odd count is padded with a copy of the last ray whose seeds are zero (exact zero
+  // terms). Distances are formed with the same fp32 operations and operands as the forward sweeps
+  // (qpair, delta_pair_rsq), so dd = dmin - delta <= 0 and v - mA <= 0 hold exactly.
   {
     (void)slots;
-    constexpr int kComb = RM_BWD_COMB_BUFS * kWaves * 8 * 64;
-    constexpr int kFields = 15;  // sweep 1: px py pz |p|^2 dmin 1/Zw b_scale mg gm.xyz d.xyz (14); sweep 2: 6
-    float* comb = L.slots;       // [RM_BWD_COMB_BUFS][kWaves][8][64] per-sphere wave sums
-    float* rayf = L.slots + kComb + wave * 64 * kFields;              // [field][64 ray slots]
-    float* gta = L.slots + kComb + kWaves * 64 * kFields + wave * 64;  // [slot] g_t sums
+    (void)live_sum;
+    (void)chunk_ctr;
+    (void)atid;
+    (void)astride;
+    constexpr int kFields = kBwdFields;  // sweep 1: px py pz |p|^2 dmin 1/Zw b_scale mg gm.xyz d.xyz (14); sweep 2: 6
+    constexpr int kWv = SPLIT ? kSplitWaves : kWaves;
+    float* rayf_all = L.slots;                     // [wave][field][64 ray slots]; after a sweep: partials
+    float* rayf = rayf_all + wave * 64 * kFields;  // this wave's rays
+    float* gta = L.slots + kWaves * 64 * kFields;  // [computing wave][source wave][64] g_t shares
+    int* nsrc = reinterpret_cast<int*>(L.misc) + 40;  // [kWaves] the sources' ray counts (sweep 1, then 2)
     const int np = a.Mpad / 2;
     const float4* R4 = reinterpret_cast<const float4*>(a.rec_buf);
     const float2* R2 = reinterpret_cast<const float2*>(R4 + 7 * (size_t)np);
     const int ngrp = (a.Mpad + 63) / 64;
-    // the block's live waves sum their per-sphere lane sums in wave order into the record
-    // ncomp = 8: sweep 1 writes the sphere's 8 columns; ncomp = 4: sweep 2 adds its (gc, gr)
-    // terms to columns 0-3 (written by sweep 1 of this block before the barrier between the sweeps)
-    auto combine = [&](const float (&v)[8], int ncomp, int grp) {
-      float* cb = comb + (RM_BWD_COMB_BUFS > 1 ? (chunk_ctr & 1) * (kWaves * 8 * 64) : 0);
+    const int nlive = __popc(alive);
+    // the packed pair (slots s, s + 1) of field f of source wave sw's image
+    auto pair = [&](int sw, int f, int s) {
+      return *reinterpret_cast<const f2*>(rayf_all + (sw * kFields + f) * 64 + s);
+    };
+    const unsigned long long below = (1ull << lane) - 1ull;
+    // this wave's units of a sweep with nsw sources: [u0, u1)
+    auto unit_range = [&](int r, int nsw, int& u0, int& u1) {
+      const int U = ngrp * nsw;
+      u0 = (r * U) / nlive;
+      u1 = ((r + 1) * U) / nlive;
+    };
+    // the block's source waves (bits) from the published counts
+    auto sources = [&]() {
+      int m = 0;
 #pragma unroll
-      for (int c = 0; c < 8; ++c)
-        if (c < ncomp) cb[(wave * 8 + c) * 64 + lane] = v[c];
+      for (int sw = 0; sw < kWv; ++sw)
+        if ((alive >> sw) & 1) m |= nsrc[sw] > 0 ? (1 << sw) : 0;
+      return __builtin_amdgcn_readfirstlane(m);
+    };
+    // Partials of the groups a wave holds only in part: slot 0 its first group, slot 1 its last,
+    // kept in registers through the sweep and written over the wave's own ray image after it
+    // (ncomp floats x 64 per slot). The wave that holds a split group's first unit adds the
+    // partials of the waves that hold its units, in order, and writes (ncomp 8) or adds to (4)
+    // the record columns.
+    // Does a wave boundary fall inside a group (a multiple of nsw units is a group boundary)?
+    auto has_split = [&](int nsw) {
+      const int U = ngrp * nsw;
+      for (int r = 1; r < nlive; ++r)
+        if (((r * U) / nlive) % nsw != 0) return true;
+      return false;
+    };
+    auto finish_split = [&](int nsw, int ncomp, const float (&p0)[8], const float (&p1)[8]) {
+      __syncthreads();  // every wave is done with the sweep's images
+      // the partials indexed by live rank: slot 0 in rows [0, nst), slot 1 in [nst, 2 nst) (a
+      // sweep-1 partial's column 7 is 0 and not stored: 14 rows fit a wave's 15-row image)
+      const int nst = ncomp == 8 ? 7 : 4;
+      float* mine = rayf_all + arank * 64 * kFields;
+#pragma unroll
+      for (int c = 0; c < 7; ++c)
+        if (c < nst) {
+          mine[c * 64 + lane] = p0[c];
+          mine[(nst + c) * 64 + lane] = p1[c];
+        }
       __syncthreads();
-      for (int e = atid; e < 64 * ncomp; e += astride) {
-        const int sl = e / ncomp, c = e - sl * ncomp;
-        if (grp * 64 + sl < a.Mpad) {
-          float* dst = rec + (long long)(grp * 64 + sl) * 8 + c;
-          const float sum = live_sum(cb + c * 64 + sl, 8 * 64);
-          *dst = ncomp == 8 ? sum : *dst + sum;
+      int u0, u1;
+      unit_range(arank, nsw, u0, u1);
+      if (u1 <= u0) return;
+      const int gl = (u1 - 1) / nsw;  // this wave's last group
+      const int kb = max(u0, gl * nsw) - gl * nsw;
+      if (kb != 0 || u1 - gl * nsw >= nsw) return;  // not the first unit of a split group
+      // this wave holds units [0, u1 - gl nsw) of group gl: its last group, or its only one
+      float acc[8];
+      const int own_slot = (u0 / nsw == gl) ? 0 : 1;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[c] = c < nst ? mine[(nst * own_slot + c) * 64 + lane] : 0.0f;
+      for (int rr = arank + 1; rr < nlive; ++rr) {  // the next waves hold the group's next units
+        int v0, v1;
+        unit_range(rr, nsw, v0, v1);
+        if (v0 >= (gl + 1) * nsw) break;
+        if (v1 <= v0) continue;
+        const float* part = rayf_all + rr * 64 * kFields;  // its first group: slot 0
+#pragma unroll
+        for (int c = 0; c < 7; ++c)
+          if (c < nst) acc[c] += part[c * 64 + lane];
+      }
+      const int j = gl * 64 + lane;
+      if (j < a.Mpad) {
+        float4* dst = reinterpret_cast<float4*>(rec + (long long)j * 8);
+        if (ncomp == 8) {
+          dst[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+          dst[1] = make_float4(acc[4], acc[5], acc[6], 0.0f);
+        } else {
+          float4 v = dst[0];
+          v.x += acc[0];
+          v.y += acc[1];
+          v.z += acc[2];
+          v.w += acc[3];
+          dst[0] = v;
         }
       }
-      if (RM_BWD_COMB_BUFS == 1) __syncthreads();  // one buffer: read by every live wave before reuse
-      ++chunk_ctr;
     };
-    // the packed pair (slots s, s + 1) of field f
-    auto pair = [&](int f, int s) { return *reinterpret_cast<const f2*>(rayf + f * 64 + s); };
-    const unsigned long long below = (1ull << lane) - 1ull;
 
     // ---- sweep 1 at p_final: colour softmax + mask soft-min + p_final(t_final)
     const unsigned long long act1 = __ballot(gm[0] != 0.0f || gm[1] != 0.0f || gm[2] != 0.0f || b_scale != 0.0f);
@@ -2305,15 +2395,24 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
 #pragma unroll
         for (int f = 0; f < 14; ++f) rayf[f * 64 + n1] = pad[f];
       }
-      gta[rank1] = 0.0f;
     }
-    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) nsrc[wave] = n1;
+#pragma unroll
+    for (int sw = 0; sw < kWv; ++sw) gta[(wave * kWaves + sw) * 64 + lane] = 0.0f;
+    __syncthreads();  // every live wave's image and count
+    const int srcs1 = sources();
+    const int nsw1 = __popc(srcs1);
+    bool split1 = false;
     {
       const f2 CL = sp(c10l), KA = sp(kappa), NCS = sp(-a.csharp);
-      const int npr1 = (n1 + 1) >> 1;
+      float p0[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, p1[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
       auto sweep1 = [&](auto clamp_tag) {
         constexpr bool CLAMP = decltype(clamp_tag)::value;
-        for (int grp = 0; grp < ngrp; ++grp) {
+        int u0, u1;
+        unit_range(arank, nsw1, u0, u1);
+        for (int u = u0; u < u1;) {
+          const int grp = u / nsw1, kb = u - grp * nsw1, ke = min(u1 - grp * nsw1, nsw1);
+          u = grp * nsw1 + ke;
           const int j = grp * 64 + lane;
           float gx = -2.0f * kPadCenter, gy = 0.0f, gz = 0.0f, cc = kPadCenter * kPadCenter, rr = 0.0f, cr = 0.0f,
                 cg = 0.0f, cbl = 0.0f;
@@ -2334,65 +2433,106 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
           const f2 GX = sp(gx), GY = sp(gy), GZ = sp(gz), CC = sp(cc), RR = sp(rr), CR = sp(cr), CG = sp(cg),
                    CB = sp(cbl), HX = sp(0.5f * gx), HY = sp(0.5f * gy), HZ = sp(0.5f * gz);
           f2 agc[3] = {sp(0.0f), sp(0.0f), sp(0.0f)}, agr = sp(0.0f), acol[3] = {sp(0.0f), sp(0.0f), sp(0.0f)};
-          for (int b = 0; b < npr1; b += 4) {  // batches of 4 pairs = 8 slots
-            float gtv[8];
+          for (int sw = 0, k = 0; sw < kWv; ++sw) {
+            if (!((srcs1 >> sw) & 1)) continue;
+            const int kk = k++;
+            if (kk < kb || kk >= ke) continue;
+            const int ns = nsrc[sw], nps = (ns + 1) >> 1;
+            float* gacc = gta + (wave * kWaves + sw) * 64;
+            for (int b = 0; b < nps; b += 4) {  // batches of 4 pairs = 8 slots
+              float gtv[8];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              if (b + u >= npr1) {  // batch slots past the last pair
-                gtv[2 * u] = gtv[2 * u + 1] = 0.0f;
-                continue;
+              for (int uu = 0; uu < 4; ++uu) {
+                if (b + uu >= nps) {  // batch slots past the last pair
+                  gtv[2 * uu] = gtv[2 * uu + 1] = 0.0f;
+                  continue;
+                }
+                const int s0 = 2 * (b + uu);
+                const f2 PX = pair(sw, 0, s0), PY = pair(sw, 1, s0), PZ = pair(sw, 2, s0), PP = pair(sw, 3, s0);
+                const f2 DM = pair(sw, 4, s0), IZ = pair(sw, 5, s0), BS = pair(sw, 6, s0), MG = pair(sw, 7, s0);
+                const f2 G0 = pair(sw, 8, s0), G1 = pair(sw, 9, s0), G2 = pair(sw, 10, s0);
+                const f2 DX = pair(sw, 11, s0), DY = pair(sw, 12, s0), DZ = pair(sw, 13, s0);
+                f2 q = fma2(PZ, GZ, fma2(PY, GY, fma2(PX, GX, PP + CC)));  // == qpair: the shade sweep's q
+                const f2 qraw = q;
+                if constexpr (CLAMP) q = clamp_q(q);
+                const f2 ir = rsq2(q);  // == delta_pair_rsq: the shade sweep's delta, and 1/rho
+                const f2 dl = q * ir - RR;
+                const f2 dd = DM - dl;  // <= 0 exactly
+                const f2 w = exp2v(dd * CL) * IZ;
+                const f2 bt = exp2v(dd * KA) * BS;
+                const f2 cgm = fma2(CB, G2, fma2(CG, G1, CR * G0));
+                const f2 gd = fma2(w * NCS, cgm - MG, bt);
+                f2 gu = gd * ir;
+                if constexpr (CLAMP) {  // clamp_min(1e-6) gate
+                  gu.x = qraw.x >= 1e-6f ? gu.x : 0.0f;
+                  gu.y = qraw.y >= 1e-6f ? gu.y : 0.0f;
+                }
+                const f2 ex = HX + PX, ey = HY + PY, ez = HZ + PZ;  // == fma2(HALF, -2c, p) = p - c
+                const f2 ngu = -gu;
+                agc[0] = fma2(ngu, ex, agc[0]);  // gc_j -= g_delta_j u_j
+                agc[1] = fma2(ngu, ey, agc[1]);
+                agc[2] = fma2(ngu, ez, agc[2]);
+                const f2 gt2 = gu * fma2(ez, DZ, fma2(ey, DY, ex * DX));  // (g_delta_j u_j) . d
+                gtv[2 * uu] = gt2.x;
+                gtv[2 * uu + 1] = gt2.y;
+                agr -= gd;
+                acol[0] = fma2(w, G0, acol[0]);
+                acol[1] = fma2(w, G1, acol[1]);
+                acol[2] = fma2(w, G2, acol[2]);
               }
-              const int s0 = 2 * (b + u);
-              const f2 PX = pair(0, s0), PY = pair(1, s0), PZ = pair(2, s0), PP = pair(3, s0);
-              const f2 DM = pair(4, s0), IZ = pair(5, s0), BS = pair(6, s0), MG = pair(7, s0);
-              const f2 G0 = pair(8, s0), G1 = pair(9, s0), G2 = pair(10, s0);
-              const f2 DX = pair(11, s0), DY = pair(12, s0), DZ = pair(13, s0);
-              f2 q = fma2(PZ, GZ, fma2(PY, GY, fma2(PX, GX, PP + CC)));  // == qpair: the shade sweep's q
-              const f2 qraw = q;
-              if constexpr (CLAMP) q = clamp_q(q);
-              const f2 ir = rsq2(q);  // == delta_pair_rsq: the shade sweep's delta, and 1/rho
-              const f2 dl = q * ir - RR;
-              const f2 dd = DM - dl;  // <= 0 exactly
-              const f2 w = exp2v(dd * CL) * IZ;
-              const f2 bt = exp2v(dd * KA) * BS;
-              const f2 cgm = fma2(CB, G2, fma2(CG, G1, CR * G0));
-              const f2 gd = fma2(w * NCS, cgm - MG, bt);
-              f2 gu = gd * ir;
-              if constexpr (CLAMP) {  // clamp_min(1e-6) gate
-                gu.x = qraw.x >= 1e-6f ? gu.x : 0.0f;
-                gu.y = qraw.y >= 1e-6f ? gu.y : 0.0f;
-              }
-              const f2 ex = HX + PX, ey = HY + PY, ez = HZ + PZ;  // == fma2(HALF, -2c, p) = p - c
-              const f2 ngu = -gu;
-              agc[0] = fma2(ngu, ex, agc[0]);  // gc_j -= g_delta_j u_j
-              agc[1] = fma2(ngu, ey, agc[1]);
-              agc[2] = fma2(ngu, ez, agc[2]);
-              const f2 gt2 = gu * fma2(ez, DZ, fma2(ey, DY, ex * DX));  // (g_delta_j u_j) . d
-              gtv[2 * u] = gt2.x;
-              gtv[2 * u + 1] = gt2.y;
-              agr -= gd;
-              acol[0] = fma2(w, G0, acol[0]);
-              acol[1] = fma2(w, G1, acol[1]);
-              acol[2] = fma2(w, G2, acol[2]);
+              const float r0 = wave_reduce8(gtv, lane);
+              const int slot = 2 * b + (lane >> 3);
+              if ((lane & 7) == 7 && slot < ns) gacc[slot] += r0;
             }
-            const float r0 = wave_reduce8(gtv, lane);
-            const int slot = 2 * b + (lane >> 3);
-            if ((lane & 7) == 7 && slot < n1) gta[slot] += r0;
           }
           const float v[8] = {agc[0].x + agc[0].y, agc[1].x + agc[1].y, agc[2].x + agc[2].y, agr.x + agr.y,
                               acol[0].x + acol[0].y, acol[1].x + acol[1].y, acol[2].x + acol[2].y, 0.0f};
-          combine(v, 8, grp);
+          if (kb == 0 && ke == nsw1) {  // every source: the group's columns, written by this wave alone
+            if (j < a.Mpad) {
+              float4* dst = reinterpret_cast<float4*>(rec + (long long)j * 8);
+              dst[0] = make_float4(v[0], v[1], v[2], v[3]);
+              dst[1] = make_float4(v[4], v[5], v[6], 0.0f);
+            }
+          } else if (grp == u0 / nsw1) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) p0[c] = v[c];
+          } else {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) p1[c] = v[c];
+          }
         }
       };
-      if (fast_f) sweep1(std::false_type{});
-      else sweep1(std::true_type{});
+      if (nsw1 == 0) {  // no ray of the block has a seed: the group columns are zeros
+        for (int grp = arank; grp < ngrp; grp += nlive)
+          if (grp * 64 + lane < a.Mpad) {
+            float4* dst = reinterpret_cast<float4*>(rec + (long long)(grp * 64 + lane) * 8);
+            dst[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            dst[1] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          }
+      } else if (fast_f) {
+        sweep1(std::false_type{});
+      } else {
+        sweep1(std::true_type{});
+      }
+      split1 = has_split(nsw1);
+      if (split1) finish_split(nsw1, 8, p0, p1);
+      else __syncthreads();  // every computing wave's g_t shares
     }
 
     // ---- sweep 2 at p_approx: t_final = t + D(p_approx) -> g_t * softmax(-k dist_a)
-    __builtin_amdgcn_wave_barrier();
-    const float gt = on1 ? gta[rank1] : 0.0f;
+    float gt = 0.0f;
+    if (on1) {
+      bool first = true;
+#pragma unroll
+      for (int w = 0; w < kWv; ++w)
+        if ((alive >> w) & 1) {
+          const float v = gta[(w * kWaves + wave) * 64 + rank1];
+          gt = first ? v : gt + v;
+          first = false;
+        }
+    }
     const float hs = gt * frcp(sA);
-    __syncthreads();  // every wave is done reading the sweep-1 ray data and combine buffers
+    if (split1) __syncthreads();  // every split partial read (the images hold them)
     const unsigned long long act2 = __ballot(hs != 0.0f);
     const int n2 = __popcll(act2), rank2 = __popcll(act2 & below);
     if (((act2 >> lane) & 1ull) != 0ull) {
@@ -2405,13 +2545,20 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
         for (int f = 0; f < 6; ++f) rayf[f * 64 + n2] = pad[f];
       }
     }
-    __builtin_amdgcn_wave_barrier();
-    {
+    if (lane == 0) nsrc[wave] = n2;
+    __syncthreads();  // every live wave's sweep-2 image and count
+    const int srcs2 = sources();
+    const int nsw2 = __popc(srcs2);
+    if (nsw2 > 0) {
       const f2 NK = sp(nkappa);
-      const int npr2 = (n2 + 1) >> 1;
+      float p0[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, p1[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
       auto sweep2 = [&](auto clamp_tag) {
         constexpr bool CLAMP = decltype(clamp_tag)::value;
-        for (int grp = 0; grp < ngrp; ++grp) {
+        int u0, u1;
+        unit_range(arank, nsw2, u0, u1);
+        for (int u = u0; u < u1;) {
+          const int grp = u / nsw2, kb = u - grp * nsw2, ke = min(u1 - grp * nsw2, nsw2);
+          u = grp * nsw2 + ke;
           const int j = grp * 64 + lane;
           float gx = -2.0f * kPadCenter, gy = 0.0f, gz = 0.0f, cc = kPadCenter * kPadCenter, kr = 0.0f;
           if (j < a.Mpad) {
@@ -2427,32 +2574,55 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
           const f2 GX = sp(gx), GY = sp(gy), GZ = sp(gz), CC = sp(cc), KR = sp(kr), HX = sp(0.5f * gx),
                    HY = sp(0.5f * gy), HZ = sp(0.5f * gz);
           f2 agc[3] = {sp(0.0f), sp(0.0f), sp(0.0f)}, agr = sp(0.0f);
-          for (int i2 = 0; i2 < npr2; ++i2) {
-            const int s0 = 2 * i2;
-            const f2 PX = pair(0, s0), PY = pair(1, s0), PZ = pair(2, s0), PP = pair(3, s0);
-            const f2 MA = pair(4, s0), HS = pair(5, s0);
-            f2 q = fma2(PZ, GZ, fma2(PY, GY, fma2(PX, GX, PP + CC)));  // == qpair: the reconnect sweep's q
-            const f2 qraw = q;
-            if constexpr (CLAMP) q = clamp_q(q);
-            const f2 r = rsq2(q);  // rho = q rsq(q) as in lse_point, 1/rho = rsq(q)
-            const f2 h = exp2v(fma2(q * r, NK, KR) - MA) * HS;  // v - mA <= 0 exactly
-            f2 hu = h * r;
-            if constexpr (CLAMP) {
-              hu.x = qraw.x >= 1e-6f ? hu.x : 0.0f;
-              hu.y = qraw.y >= 1e-6f ? hu.y : 0.0f;
+          for (int sw = 0, k = 0; sw < kWv; ++sw) {
+            if (!((srcs2 >> sw) & 1)) continue;
+            const int kk = k++;
+            if (kk < kb || kk >= ke) continue;
+            const int nps = (nsrc[sw] + 1) >> 1;
+            for (int i2 = 0; i2 < nps; ++i2) {
+              const int s0 = 2 * i2;
+              const f2 PX = pair(sw, 0, s0), PY = pair(sw, 1, s0), PZ = pair(sw, 2, s0), PP = pair(sw, 3, s0);
+              const f2 MA = pair(sw, 4, s0), HS = pair(sw, 5, s0);
+              f2 q = fma2(PZ, GZ, fma2(PY, GY, fma2(PX, GX, PP + CC)));  // == qpair: the reconnect sweep's q
+              const f2 qraw = q;
+              if constexpr (CLAMP) q = clamp_q(q);
+              const f2 r = rsq2(q);  // rho = q rsq(q) as in lse_point, 1/rho = rsq(q)
+              const f2 h = exp2v(fma2(q * r, NK, KR) - MA) * HS;  // v - mA <= 0 exactly
+              f2 hu = h * r;
+              if constexpr (CLAMP) {
+                hu.x = qraw.x >= 1e-6f ? hu.x : 0.0f;
+                hu.y = qraw.y >= 1e-6f ? hu.y : 0.0f;
+              }
+              agc[0] = fma2(-hu, HX + PX, agc[0]);
+              agc[1] = fma2(-hu, HY + PY, agc[1]);
+              agc[2] = fma2(-hu, HZ + PZ, agc[2]);
+              agr -= h;
             }
-            agc[0] = fma2(-hu, HX + PX, agc[0]);
-            agc[1] = fma2(-hu, HY + PY, agc[1]);
-            agc[2] = fma2(-hu, HZ + PZ, agc[2]);
-            agr -= h;
           }
           const float v[8] = {agc[0].x + agc[0].y, agc[1].x + agc[1].y, agc[2].x + agc[2].y, agr.x + agr.y,
                               0.0f, 0.0f, 0.0f, 0.0f};
-          combine(v, 4, grp);
+          if (kb == 0 && ke == nsw2) {  // added to the group's sweep-1 columns 0-3
+            if (j < a.Mpad) {
+              float4* dst = reinterpret_cast<float4*>(rec + (long long)j * 8);
+              float4 o = dst[0];
+              o.x += v[0];
+              o.y += v[1];
+              o.z += v[2];
+              o.w += v[3];
+              dst[0] = o;
+            }
+          } else if (grp == u0 / nsw2) {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) p0[c] = v[c];
+          } else {
+#pragma unroll
+            for (int c = 0; c < 8; ++c) p1[c] = v[c];
+          }
         }
       };
       if (fast_a) sweep2(std::false_type{});
       else sweep2(std::true_type{});
+      if (has_split(nsw2)) finish_split(nsw2, 4, p0, p1);
     }
   }
   __syncthreads();
@@ -3267,12 +3437,16 @@ int fail(rm_context* ctx, int code, const char* fmt, ...) {
 // the pixel order of setup_ray. Built once per image size.
 int ensure_block_order(rm_context* ctx, int tx, int ty, int sub) {
   if (ctx->block_order && ctx->order_tx == tx && ctx->order_ty == ty && ctx->order_sub == sub) return RM_OK;
-  // sub = ray blocks per 16x16 tile: 1 (256-ray blocks) or 4 (8x8 quadrants: 64-ray blocks, split)
+  // sub = ray blocks per 16x16 tile: 1 (256-ray blocks), 4 (8x8 quadrants: 64-ray split blocks),
+  // 8 (8x4 halves of the quadrants: 32-ray split blocks) or 16 (8x2 quarters: 16-ray split blocks)
   std::vector<int> ord((size_t)tx * ty * sub);
   for (size_t i = 0; i < ord.size(); ++i) ord[i] = (int)i;
   auto key = [&](int i) {  // twice the pixel offset of the block centre from the image centre
     const int tile = i / sub, q = i % sub;
-    const long long ox = sub == 1 ? 16 : 16 * (q & 1) + 8, oy = sub == 1 ? 16 : 16 * (q >> 1) + 8;
+    const int per_quad = sub / 4, quad = sub == 1 ? 0 : q / per_quad, part = sub == 1 ? 0 : q % per_quad;
+    const long long rows = sub == 1 ? 16 : 8 / per_quad;  // pixel rows of one block inside its quadrant
+    const long long ox = sub == 1 ? 16 : 16 * (quad & 1) + 8,
+                    oy = sub == 1 ? 16 : 16 * (quad >> 1) + 2 * rows * part + rows;
     const long long dx = 32LL * (tile % tx) + ox - 16LL * tx, dy = 32LL * (tile / tx) + oy - 16LL * ty;
     return dx * dx + dy * dy;
   };
@@ -3759,7 +3933,7 @@ int run(rm_context* ctx, const Call& c) {
       split = (M >= kSplitMinSpheres && n_all <= kSplitMaxRays) || (M >= kSplitMinSpheresWide && n_all <= kSplitMaxRaysWide);
   }
   a.split = split ? 1 : 0;
-  const int rpb = split ? 64 : kBlock;  // rays per block
+  const int rpb = split ? kSplitRays : kBlock;  // rays per block
   a.cull = ((c.march->flags & RM_MARCH_SKIP_ESCAPED) != 0 && mask_vanishes && !c.t_out && !c.dbg && !split) ? 1 : 0;
   a.cull_min_d = c.mode == kRender ? 50.0f : std::max(50.0f, 160.0f / (a.msharp * 1.44269504f));
   a.lse_slack = (float)(std::log((double)M) / (double)a.k * (1.0 + 1e-6)) + 1e-7f;
@@ -3929,7 +4103,7 @@ int run(rm_context* ctx, const Call& c) {
       int* lists[2] = {nullptr, nullptr};
       int* counts[2] = {nullptr, nullptr};
       if (cont) {
-        const long long rays = nb * 64;
+        const long long rays = nb * kSplitRays;
         const size_t need = (size_t)(6 * rays + 2 * nb) * sizeof(float) + (size_t)(2 * nb + 16) * sizeof(int);
         if (ctx->cont_bytes < need) {
           if (ctx->cont_buf) RM_HIP(ctx, hipFree(ctx->cont_buf));
@@ -3984,7 +4158,10 @@ int run(rm_context* ctx, const Call& c) {
 
 extern "C" {
 
-const char* rm_version(void) { return "burn_raymarching_amd 0.1.0 (gfx950)"; }
+#ifndef RM_SOURCE_SHA
+#define RM_SOURCE_SHA "unknown"  // _build.py passes the sha256 of the kernel sources
+#endif
+const char* rm_version(void) { return "burn_raymarching_amd 0.1.0 (gfx950) src " RM_SOURCE_SHA; }
 
 int rm_create(int32_t device, void* stream, rm_context** out_ctx) {
   if (!out_ctx) return RM_ERR_INVALID_ARG;

@@ -149,6 +149,8 @@ typedef struct rm_grads {
 } rm_grads;
 
 /* ---- context --------------------------------------------------------------- */
+/* "burn_raymarching_amd <version> (gfx950) src <hash>": <hash> = the first 16 hex digits of the
+ * sha256 of the kernel sources the library was built from (burn_raymarching_amd/_build.py). */
 const char* rm_version(void);
 /* stream: a hipStream_t (NULL = the null stream). */
 int rm_create(int32_t device, void* stream, rm_context** out_ctx);

@@ -150,23 +150,27 @@ typedef struct rmh_collective {
   /* Nullable. The driver's only way of waiting for its stream while collectives may be in
    * flight (instead of hipStreamSynchronize): returns RMH_OK once the stream drained, or an error
    * when it did not within the implementation's timeout -- the RCCL one then aborts its
-   * communicator, so a rank whose peer died fails instead of spinning forever. */
+   * communicator, so a rank whose peer died fails instead of spinning forever. rmh_train calls it
+   * on every rank at least every 32 steps (and at stage ends and loss reads), so the queued work a
+   * wait covers -- what its timeout must allow for -- is at most 32 steps. */
   int (*wait)(void* state, void* stream);
 } rmh_collective;
 /* RCCL communicator of rank `rank` of `world` on HIP device `device`. Rank 0 creates the
  * ncclUniqueId and publishes it at id_path (rmh_rendezvous_publish); the other ranks wait up to
  * timeout_s seconds for it (rmh_rendezvous_read) -- however late they start; rank 0 removes the
- * file once every rank has joined. run_id (nullable: env RMH_RUN_ID, else TORCHELASTIC_RUN_ID,
- * else "") tags the file, so a file left by an earlier run with another id is never used; with an
- * empty id the launcher must give each run a fresh path or remove the file before starting the
- * ranks. timeout_s is also the watchdog of `wait`. id_path may be NULL when world == 1. */
+ * file once every rank has joined. run_id (nullable: env RMH_RUN_ID, else TORCHELASTIC_RUN_ID)
+ * tags the file, so a file left by an earlier run with another id is never used; with world > 1 it
+ * must name this run -- an empty id or torchrun's default "none" is refused (RMH_ERR_INVALID_ARG,
+ * before any GPU call): a stale file of a crashed run would pass for such a run's. timeout_s is
+ * also the watchdog of `wait`. id_path may be NULL when world == 1. */
 int rmh_collective_rccl_create(int32_t rank, int32_t world, int32_t device, const char* id_path, const char* run_id,
                                double timeout_s, rmh_collective* out);
 void rmh_collective_rccl_destroy(rmh_collective* c);
 /* The file rendezvous of rmh_collective_rccl_create, on any payload: publish writes
  * [magic | run id | size | blob] to a temporary name and renames it to path (a stale file at path
  * is removed first); read polls path until a complete file with the same run id and payload size
- * appears (RMH_ERR_IO after timeout_s seconds, naming what the file there held). run_id as above. */
+ * appears (RMH_ERR_IO after timeout_s seconds, naming what the file there held). run_id as above
+ * (an empty or "none" id: RMH_ERR_INVALID_ARG). */
 int rmh_rendezvous_publish(const char* path, const char* run_id, const void* blob, int64_t size);
 int rmh_rendezvous_read(const char* path, const char* run_id, void* blob, int64_t size, double timeout_s);
 
@@ -193,8 +197,11 @@ typedef struct rmh_train_config {
    * prune_and_split and broadcasts the next generation (its size, then its 7M'+4 raw params);
    * only rank 0 logs and writes files. Every rank ends with the same parameters. */
   const rmh_collective* comm;
-  /* Growth knobs of prune_and_split (rmh_prune_and_split_ex): 1, 0.05 and 0 (no cap), the
-   * reference rule. */
+  /* Growth knobs of prune_and_split (rmh_prune_and_split_ex). A zeroed struct gets the reference
+   * rule (training.rs:185-188): split_scale 0 = 1 (the threshold 0.25 * 0.65^stage times this),
+   * split_move 0 = 0.05 (the minimum move); a negative value drops that condition (both negative:
+   * every surviving sphere splits -- the growth runs of configs[4], rm_train --split-all);
+   * max_spheres 0 = no cap. rmh_train_config_default sets 1, 0.05, 0. */
   float split_scale;
   float split_move;
   int32_t max_spheres;

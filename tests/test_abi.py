@@ -81,3 +81,14 @@ def test_packed_views(native):
 def test_built_for_gfx950(native):
     data = open(native.LIB_PATH, "rb").read()
     assert b"gfx950" in data
+
+
+def test_shipped_library_matches_sources(native):
+    """The in-tree libraymarch_hip.so (the one that travels to the GPU box) was built from the
+    kernel sources in this tree: rm_version() carries their sha256 prefix (_build.py)."""
+    from burn_raymarching_amd import _build
+    if os.environ.get("RM_LIB_PATH"):
+        pytest.skip("RM_LIB_PATH names another library")
+    want = _build.source_hash()
+    assert native.lib().rm_version().decode().endswith("src " + want)
+    assert _build.lib_source_hash(native.LIB_PATH) == want

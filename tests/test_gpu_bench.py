@@ -54,3 +54,12 @@ def test_bench_without_kernel_timing():
     d = _bench("--steps", "2", "--warmup", "1", "--width", "64", "--height", "64", "--views-per-gpu", "1",
                "--cpu-baseline", "off", "--kernel-timing", "off")
     assert d["value"] > 0 and d["roofline"] is None and d["cpu_baseline"] is None
+
+
+def test_graph_refuses_rotating_views():
+    """--graph captures one step: its views are frozen into the graph, so a run whose views rotate
+    over a larger ring is refused rather than timed on other work than its eager steps."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--graph", "on", "--views-per-gpu", "2",
+                          "--ring", "10", "--width", "64", "--height", "64", "--steps", "2", "--cpu-baseline", "off"],
+                         cwd=ROOT, capture_output=True, text=True, timeout=110)
+    assert out.returncode != 0 and "--graph on needs the same views every step" in out.stderr, out.stderr[-2000:]

@@ -114,3 +114,30 @@ def test_t_march_contract_against_oracle(mods, oracle):
     # where the ray still sees the scene (reference mask not negligible) t is the reference's
     seen = np.abs(ref).max(axis=1) > 1e-6
     assert np.all(close[seen])
+
+
+@pytest.mark.parametrize("steps", [40, 128])
+@pytest.mark.parametrize("small", ["0", "1"])
+def test_receding_rays_stay_finite(mods, oracle, monkeypatch, steps, small):
+    """A view that looks away from the scene: where the reference's fp32 march
+    loses the rays at 128 steps (tests/test_oracle.py::test_reference_f32_march_breaks_for_receding_rays)
+    the kernels -- general and small-scene -- return the fp64 restatement's exact 0 through the t
+    cap: forward with t_march, and the train step's loss and sphere gradients, exit on and off."""
+    torch, model, render = mods
+    monkeypatch.setenv("RM_SMALL", small)
+    sc = model.scene_tensors(model.synthetic_scene(16, seed=0), "cuda")
+    eye = np.float32([0.0, 0.5, 2.5])
+    o, d = oracle.camera_rays(8, 8, eye, eye * 2.0, 50.0, precision="f32")
+    dev = lambda x: torch.from_numpy(np.ascontiguousarray(x, np.float32)).cuda()  # noqa: E731
+    out, t = render.render_diff_forward(dev(o), dev(d), sc, 32.0, steps, return_t=True)
+    assert torch.isfinite(t).all() and float(t.max()) <= 1e15
+    assert float(out.abs().max()) == 0.0
+    tgt = torch.full_like(out, 0.25)
+    for exit_off in ("1", "0"):
+        monkeypatch.setenv("RM_NO_EARLY_EXIT", exit_off)
+        loss, g, out2 = render.train_step(dev(o), dev(d), tgt, sc, 32.0, 0.5, steps, with_out=True)
+        torch.cuda.synchronize()
+        assert torch.isfinite(loss).all() and float(out2.abs().max()) == 0.0
+        for key in ("centers", "colors", "radius"):
+            assert float(g[key].abs().max()) == 0.0, key
+        assert all(torch.isfinite(v).all() for v in g.values())

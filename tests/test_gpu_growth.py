@@ -3,7 +3,7 @@ fp32 SDF" -- grown through prune_and_split (training.rs:87-238, train.rs:306-328
 driver, at a reduced size:
 
   * rmh_train on the reference's own targets (tests/golden: data/cameras.json + target PNGs) with
-    128 march steps, fp16 colours and the growth knobs split_scale = split_move = 0 (every sphere
+    128 march steps, fp16 colours and the growth knobs split_scale = split_move = -1 (every sphere
     that survives pruning splits; rmh_prune_and_split_ex): the model grows 7 -> 14 -> ... past 32,
     256 and 512 spheres, so the run itself crosses the small -> general kernel switch (M > 32) and
     the split-march thresholds (256 / 512 spheres) at its batch of 16,384 rays, with the split
@@ -35,7 +35,7 @@ def grown():
     from burn_raymarching_amd import host
     gens = []
     cfg = host.train_config(cameras_json=os.path.join(GOLDEN, "cameras.json"), out_dir=None, log_every=0, previews=0,
-                            stages=8, steps_per_stage=25, march_steps=S, seed=11, split_scale=0.0, split_move=0.0,
+                            stages=8, steps_per_stage=25, march_steps=S, seed=11, split_scale=-1.0, split_move=-1.0,
                             color_f16=1)
     host.on_generation(cfg, lambda stage, m, raw: gens.append((stage, m, raw)))
     res, raw = host.train(cfg)

@@ -129,3 +129,25 @@ def test_gather_rays_matches_indexing():
         o = o.cpu()
         assert torch.equal(o[ok], s[idx[ok].long()])
         assert not o[~ok].any()
+
+
+def test_zeroed_config_trains_the_reference_rule(H):
+    """a zero-initialised rmh_train_config (a binding that fills only the fields it
+    knows and never calls rmh_train_config_default) trains with the reference split rule
+    (training.rs:185-188) -- bit for bit the default config's run -- and growth needs the explicit
+    negative knobs (rm_train --split-all)."""
+    # a small learning rate: no sphere moves the reference's 0.05 (training.rs:188), so the reference
+    # rule splits none and split-all splits every one
+    kw = dict(cameras_json=os.path.join(GOLDEN, "cameras.json"), out_dir=None, log_every=0, previews=0, stages=3,
+              steps_per_stage=30, batch=4096, seed=5, base_lr=0.001)
+    ref = H.train_config(**kw)
+    zero = H.RmhTrainConfig()  # every field 0 / NULL
+    for f in ("cameras_json", "width", "height", "stages", "steps_per_stage", "batch", "march_steps", "max_smooth",
+              "base_lr", "weight_decay", "seed", "device"):
+        setattr(zero, f, getattr(ref, f))
+    assert zero.split_scale == 0.0 and zero.split_move == 0.0 and zero.max_spheres == 0
+    r1, raw1 = H.train(ref)
+    r2, raw2 = H.train(zero)
+    assert r1.num_spheres == r2.num_spheres and np.array_equal(raw1, raw2)
+    r3, _ = H.train(H.train_config(**kw, split_scale=-1.0, split_move=-1.0))
+    assert r3.num_spheres > r1.num_spheres

@@ -86,7 +86,7 @@ def _worker(rank, world, port, out_dir, grow=False):
     cfg = _cfg(H)
     if grow:  # configs[4]-style growth: every surviving sphere splits, 128 march steps, fp16 colours
         cfg.stages, cfg.steps_per_stage, cfg.march_steps = 8, 6, 128
-        cfg.split_scale, cfg.split_move, cfg.color_f16 = 0.0, 0.0, 1
+        cfg.split_scale, cfg.split_move, cfg.color_f16 = -1.0, -1.0, 1
     cfg.comm = ctypes.pointer(comm)
     res, raw = H.train(cfg)
     np.save(os.path.join(out_dir, f"raw{rank}.npy"), raw)

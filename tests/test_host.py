@@ -358,3 +358,25 @@ def test_rendezvous_rejects_other_runs_file(H, tmp_path):
         assert H.rendezvous_read(path, None, 16, 1.0) == b"y" * 16
     finally:
         del os.environ["RMH_RUN_ID"]
+
+
+def test_rendezvous_refuses_unnamed_runs(H, tmp_path, monkeypatch):
+    """with an empty run id, or torchrun's default 'none', a file a crashed run left at
+    the same path would pass for this run's and a late rank would join a dead ncclUniqueId. The
+    rendezvous refuses such ids on both sides, and rmh_collective_rccl_create refuses them for
+    world > 1 before any GPU call (so this runs on the CPU)."""
+    path = str(tmp_path / "id")
+    monkeypatch.delenv("RMH_RUN_ID", raising=False)
+    monkeypatch.delenv("TORCHELASTIC_RUN_ID", raising=False)
+    with pytest.raises(H.HostError, match="needs a run id"):
+        H.rendezvous_publish(path, None, b"z" * 16)
+    with pytest.raises(H.HostError, match="needs a run id"):
+        H.rendezvous_publish(path, "", b"z" * 16)
+    H.rendezvous_publish(path, "crashed-run", b"z" * 16)  # a stale file of an earlier run
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "none")
+    with pytest.raises(H.HostError, match="needs a run id"):
+        H.rendezvous_read(path, None, 16, 0.2)
+    with pytest.raises(H.HostError, match="rank 1: .*needs a run id"):
+        H.rccl_collective(1, 2, 0, path)
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "crashed-run")  # an id that names the run is taken
+    assert H.rendezvous_read(path, None, 16, 1.0) == b"z" * 16

@@ -185,3 +185,23 @@ def test_fp32_gradient_error_within_gpu_bounds(oracle):
     _, _, g64 = oracle.train_step(o64, d64, tg.astype(np.float64), sc, 64, 32.0, 0.25)
     _, _, g32 = oracle.train_step(o, d, tg, sc, 64, 32.0, 0.25, precision="f32")
     within(g32, g64, "train")
+
+
+def test_reference_f32_march_breaks_for_receding_rays(oracle):
+    """The reference's fp32 arithmetic (the fp32 reference-order restatement of renderer_diff.rs:
+    22-26 over scene.rs:66-72 / sdf.rs:30-44) loses a ray that leaves the scene radially once
+    |p|^2 overflows (t about doubles every step: near step 65): t becomes inf, and the pixel turns
+    NaN or, as here where fmax(NaN, 1e-8) = 1e-8 stands in for clamp_min, spuriously non-zero. The
+    fp64 restatement stays finite with the pixel exactly 0. The HIP kernels cap t at 1e15 and
+    return exact 0 (INTEGRATION.md §6; tests/test_gpu_early_exit.py::test_receding_rays_stay_finite)."""
+    from burn_raymarching_amd.model import synthetic_scene
+    sc = synthetic_scene(16, seed=0)
+    eye = np.float32([0.0, 0.5, 2.5])
+    o32, d32 = oracle.camera_rays(8, 8, eye, eye * 2.0, 50.0, precision="f32")  # looking away
+    short, t_short = oracle.render_diff(o32, d32, sc, 40, 32.0, precision="f32", with_t=True)
+    assert np.isfinite(t_short).all() and np.abs(short).max() == 0.0
+    long32, t32 = oracle.render_diff(o32, d32, sc, 128, 32.0, precision="f32", with_t=True)
+    assert not np.isfinite(t32).any()
+    assert np.isnan(long32).any() or np.abs(long32).max() > 0.0
+    long64 = oracle.render_diff(o32.astype(np.float64), d32.astype(np.float64), sc, 128, 32.0, precision="f64")
+    assert np.isfinite(long64).all() and np.abs(long64).max() == 0.0

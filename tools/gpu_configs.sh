@@ -45,7 +45,7 @@ grow() {
   mkdir -p $G/data
   timeout -k 10 120 burn_raymarching_amd/lib/rm_train generate --out $G/data --prefix "" --size 512x512 > $G/generate.log 2>&1 && \
   timeout -k 10 600 burn_raymarching_amd/lib/rm_train train --cameras $G/data/cameras.json --out $G --size 512x512 \
-    --march-steps 128 --color-f16 --stages 11 --steps 100 --split-scale 0 --split-move 0 --max-spheres 4096 \
+    --march-steps 128 --color-f16 --stages 11 --steps 100 --split-all --max-spheres 4096 \
     --log-every 100 --no-previews > $G/train.log 2>&1 || { tail $G/train.log; return 1; }
   GM=$(python3 -c "import json; print(len(json.load(open('$G/scene.json'))['radii']))")
   grep -E "Stage|Next N|num_spheres" $G/train.log
