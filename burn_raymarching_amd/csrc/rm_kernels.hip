@@ -2297,17 +2297,19 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     const float4* R4 = reinterpret_cast<const float4*>(a.rec_buf);
     const float2* R2 = reinterpret_cast<const float2*>(R4 + 7 * (size_t)np);
     const int ngrp = (a.Mpad + 63) / 64;
-    const int nlive = __popc(alive);
+    // The computing waves of a sweep: the block's source waves -- a set that does not depend on
+    // which rayless waves left the march early, so the partition and every sum order are the same
+    // with the early exit on and off -- or, in a split block, its waves (alive together).
     // the packed pair (slots s, s + 1) of field f of source wave sw's image
     auto pair = [&](int sw, int f, int s) {
       return *reinterpret_cast<const f2*>(rayf_all + (sw * kFields + f) * 64 + s);
     };
     const unsigned long long below = (1ull << lane) - 1ull;
     // this wave's units of a sweep with nsw sources: [u0, u1)
-    auto unit_range = [&](int r, int nsw, int& u0, int& u1) {
+    auto unit_range = [&](int r, int nsw, int ncw, int& u0, int& u1) {
       const int U = ngrp * nsw;
-      u0 = (r * U) / nlive;
-      u1 = ((r + 1) * U) / nlive;
+      u0 = (r * U) / ncw;
+      u1 = ((r + 1) * U) / ncw;
     };
     // the block's source waves (bits) from the published counts
     auto sources = [&]() {
@@ -2323,27 +2325,31 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     // partials of the waves that hold its units, in order, and writes (ncomp 8) or adds to (4)
     // the record columns.
     // Does a wave boundary fall inside a group (a multiple of nsw units is a group boundary)?
-    auto has_split = [&](int nsw) {
+    auto has_split = [&](int nsw, int ncw) {
       const int U = ngrp * nsw;
-      for (int r = 1; r < nlive; ++r)
-        if (((r * U) / nlive) % nsw != 0) return true;
+      for (int r = 1; r < ncw; ++r)
+        if (((r * U) / ncw) % nsw != 0) return true;
       return false;
     };
-    auto finish_split = [&](int nsw, int ncomp, const float (&p0)[8], const float (&p1)[8]) {
+    auto finish_split = [&](int nsw, int ncw, int crank, bool in, int ncomp, const float (&p0)[8],
+                            const float (&p1)[8]) {
       __syncthreads();  // every wave is done with the sweep's images
       // the partials indexed by live rank: slot 0 in rows [0, nst), slot 1 in [nst, 2 nst) (a
       // sweep-1 partial's column 7 is 0 and not stored: 14 rows fit a wave's 15-row image)
       const int nst = ncomp == 8 ? 7 : 4;
-      float* mine = rayf_all + arank * 64 * kFields;
+      float* mine = rayf_all + crank * 64 * kFields;  // by computing rank
+      if (in) {
 #pragma unroll
-      for (int c = 0; c < 7; ++c)
-        if (c < nst) {
-          mine[c * 64 + lane] = p0[c];
-          mine[(nst + c) * 64 + lane] = p1[c];
-        }
+        for (int c = 0; c < 7; ++c)
+          if (c < nst) {
+            mine[c * 64 + lane] = p0[c];
+            mine[(nst + c) * 64 + lane] = p1[c];
+          }
+      }
       __syncthreads();
+      if (!in) return;
       int u0, u1;
-      unit_range(arank, nsw, u0, u1);
+      unit_range(crank, nsw, ncw, u0, u1);
       if (u1 <= u0) return;
       const int gl = (u1 - 1) / nsw;  // this wave's last group
       const int kb = max(u0, gl * nsw) - gl * nsw;
@@ -2353,9 +2359,9 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       const int own_slot = (u0 / nsw == gl) ? 0 : 1;
 #pragma unroll
       for (int c = 0; c < 8; ++c) acc[c] = c < nst ? mine[(nst * own_slot + c) * 64 + lane] : 0.0f;
-      for (int rr = arank + 1; rr < nlive; ++rr) {  // the next waves hold the group's next units
+      for (int rr = crank + 1; rr < ncw; ++rr) {  // the next waves hold the group's next units
         int v0, v1;
-        unit_range(rr, nsw, v0, v1);
+        unit_range(rr, nsw, ncw, v0, v1);
         if (v0 >= (gl + 1) * nsw) break;
         if (v1 <= v0) continue;
         const float* part = rayf_all + rr * 64 * kFields;  // its first group: slot 0
@@ -2402,14 +2408,16 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     __syncthreads();  // every live wave's image and count
     const int srcs1 = sources();
     const int nsw1 = __popc(srcs1);
+    const int cmask1 = SPLIT ? alive : srcs1, ncw1 = __popc(cmask1), crank1 = __popc(cmask1 & ((1 << wave) - 1));
+    const bool in1 = ((cmask1 >> wave) & 1) != 0;
     bool split1 = false;
     {
       const f2 CL = sp(c10l), KA = sp(kappa), NCS = sp(-a.csharp);
       float p0[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, p1[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
       auto sweep1 = [&](auto clamp_tag) {
         constexpr bool CLAMP = decltype(clamp_tag)::value;
-        int u0, u1;
-        unit_range(arank, nsw1, u0, u1);
+        int u0 = 0, u1 = 0;
+        if (in1) unit_range(crank1, nsw1, ncw1, u0, u1);
         for (int u = u0; u < u1;) {
           const int grp = u / nsw1, kb = u - grp * nsw1, ke = min(u1 - grp * nsw1, nsw1);
           u = grp * nsw1 + ke;
@@ -2503,7 +2511,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
         }
       };
       if (nsw1 == 0) {  // no ray of the block has a seed: the group columns are zeros
-        for (int grp = arank; grp < ngrp; grp += nlive)
+        for (int grp = arank; grp < ngrp; grp += __popc(alive))
           if (grp * 64 + lane < a.Mpad) {
             float4* dst = reinterpret_cast<float4*>(rec + (long long)(grp * 64 + lane) * 8);
             dst[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -2514,8 +2522,8 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       } else {
         sweep1(std::true_type{});
       }
-      split1 = has_split(nsw1);
-      if (split1) finish_split(nsw1, 8, p0, p1);
+      split1 = nsw1 > 0 && has_split(nsw1, ncw1);
+      if (split1) finish_split(nsw1, ncw1, crank1, in1, 8, p0, p1);
       else __syncthreads();  // every computing wave's g_t shares
     }
 
@@ -2525,7 +2533,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       bool first = true;
 #pragma unroll
       for (int w = 0; w < kWv; ++w)
-        if ((alive >> w) & 1) {
+        if ((cmask1 >> w) & 1) {
           const float v = gta[(w * kWaves + wave) * 64 + rank1];
           gt = first ? v : gt + v;
           first = false;
@@ -2549,13 +2557,15 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     __syncthreads();  // every live wave's sweep-2 image and count
     const int srcs2 = sources();
     const int nsw2 = __popc(srcs2);
+    const int cmask2 = SPLIT ? alive : srcs2, ncw2 = __popc(cmask2), crank2 = __popc(cmask2 & ((1 << wave) - 1));
+    const bool in2 = ((cmask2 >> wave) & 1) != 0;
     if (nsw2 > 0) {
       const f2 NK = sp(nkappa);
       float p0[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, p1[8] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
       auto sweep2 = [&](auto clamp_tag) {
         constexpr bool CLAMP = decltype(clamp_tag)::value;
-        int u0, u1;
-        unit_range(arank, nsw2, u0, u1);
+        int u0 = 0, u1 = 0;
+        if (in2) unit_range(crank2, nsw2, ncw2, u0, u1);
         for (int u = u0; u < u1;) {
           const int grp = u / nsw2, kb = u - grp * nsw2, ke = min(u1 - grp * nsw2, nsw2);
           u = grp * nsw2 + ke;
@@ -2622,7 +2632,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       };
       if (fast_a) sweep2(std::false_type{});
       else sweep2(std::true_type{});
-      if (has_split(nsw2)) finish_split(nsw2, 4, p0, p1);
+      if (has_split(nsw2, ncw2)) finish_split(nsw2, ncw2, crank2, in2, 4, p0, p1);
     }
   }
   __syncthreads();

@@ -137,6 +137,13 @@ def analyse(tr, bins=40, steps=0):
         tot = m_all.sum() + p_all.sum() + b_all.sum()
         print(f"summed wave time: march {m_all.sum() / tot:.3f}, post-march forward {p_all.sum() / tot:.3f}, "
               f"backward {b_all.sum() / tot:.3f} (of {tot / 1e3:.1f} wave-ms)")
+        if tr.shape[1] >= 12:  # march steps per path over every wave (which share takes the clamped sweep)
+            pw = tr[:, 7].astype(np.uint64)
+            tot_paths = [int(((pw >> np.uint64(16 * k)) & np.uint64(0xFFFF)).sum()) for k in range(4)]
+            tot_paths.append(int(tr[:, 9].astype(np.int64).sum()))
+            n = max(sum(tot_paths), 1)
+            print("march steps by path (none fast, none clamped, fixed fast, fixed clamped, vector): "
+                  + " ".join(f"{v} ({v / n:.3f})" for v in tot_paths))
         order = np.argsort(-dur)[:12]
         print(" slowest waves: total  march  post  bwd (us)  steps  us/step  SIMD-sharing"
               + ("  paths(none f/c, fixed f/c, vector)  lse-cycles/step  march-cycles/step" if tr.shape[1] >= 12 else ""))
