@@ -206,7 +206,7 @@ struct KArgs {
   // rays still march at step cont_cap saves its march state, appends its logical block to
   // cont_list_w and ends; a launch with cont_resume = that step runs the saved blocks
   // (cont_list[0..*cont_count)) from there (and may defer again at its own cont_cap).
-  // cont_state: [6][cont_rays] per ray (t, lb, D_prev, t one and two steps back, gone) then
+  // cont_state: [7][cont_rays] per ray (t, lb, D_prev, t one and two steps back, gone, rho_lb) then
   // [blocks][2] per block (choice history, steps saved).
   int cont_cap, cont_resume;
   float* cont_state;
@@ -263,12 +263,14 @@ __host__ __device__ inline size_t esc_offset(int npairs, int nprep) {
   const size_t nrb = (size_t)npairs / 8;
   return tiles_offset(npairs, nprep) + nrb * 64 * 16 + nrb * 32 * sizeof(float);
 }
-// Then the per-view origin steps of camera mode (write_origins): RM_MAX_VIEWS_PER_CALL floats.
+// Then the per-view origin steps of camera mode (write_origins): RM_MAX_VIEWS_PER_CALL floats,
+// then per view a lower bound on the eye's distance to the nearest sphere centre (the march's
+// clamp-free proof, rho_lb in rm_ray_kernel): RM_MAX_VIEWS_PER_CALL floats.
 __host__ __device__ inline size_t origin_offset(int npairs, int nprep) {
   return esc_offset(npairs, nprep) + kEscTab * sizeof(float);
 }
 __host__ __device__ inline size_t rec_bytes(int npairs, int nprep) {
-  return origin_offset(npairs, nprep) + RM_MAX_VIEWS_PER_CALL * sizeof(float);
+  return origin_offset(npairs, nprep) + 2 * RM_MAX_VIEWS_PER_CALL * sizeof(float);
 }
 
 struct Lds {  // the sphere records (global, scalar-loaded) plus the kernel's LDS scratch
@@ -1061,6 +1063,25 @@ __device__ void write_origins(const KArgs& a, const float4& S00, const float4& S
     else if (a.mfma && shift_fixed_ok && psq(p) <= 1e10f)
       D = march_d_fixed<true>(p, kappa, inv_kappa, kr_first, S00, S10, Aq, Wq, nq, xa, xb, xs, lane, comb, wave);
     if (lane == 0 && wave == 0) orig[v] = D;
+    // the eye's distance to the nearest sphere centre (direct form), rounded down by a relative
+    // 1e-6 and 1e-6 (1 + |eye|) against the fp32 rounding of the eye and of the centres' offsets
+    float m2 = INFINITY;
+    for (int j = (int)threadIdx.x; j < a.M; j += (int)blockDim.x) {
+      const float dx = p[0] - a.centers[3 * j], dy = p[1] - a.centers[3 * j + 1], dz = p[2] - a.centers[3 * j + 2];
+      m2 = fminf(m2, fmaf(dz, dz, fmaf(dy, dy, dx * dx)));
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) m2 = fminf(m2, __shfl_xor(m2, off));
+    if constexpr (PAR) {
+      __shared__ float wmin[kSplitWaves];
+      if (lane == 0) wmin[wave] = m2;
+      __syncthreads();
+#pragma unroll
+      for (int w = 0; w < kSplitWaves; ++w) m2 = fminf(m2, wmin[w]);
+    }
+    if (lane == 0 && wave == 0)
+      orig[RM_MAX_VIEWS_PER_CALL + v] =
+          sqrtf(m2) * (1.0f - 1e-6f) - 1e-6f * (1.0f + fabsf(p[0]) + fabsf(p[1]) + fabsf(p[2]));
   }
 }
 
@@ -1628,7 +1649,21 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   // Rays proven to escape (`gone`, see the march) no longer take part in the wave-uniform
   // choices: their outputs and gradient terms are exactly 0 whatever they compute.
   bool gone = false;
-  auto all_safe = [&](float dist_lb) { return __all(dist_lb + rmin >= kSafeRho || gone) != 0; };
+  // A second proof per ray (camera mode): rho_lb, a lower bound on the distance to the nearest
+  // sphere CENTRE -- the eye's (write_origins), less the path marched since (every centre distance
+  // is 1-Lipschitz along the ray). Where the soft-min runs far below the hard min (small k: at
+  // k = 5 by up to ln(M)/k = 1.1) the scene-distance bound above fails inside the scene long
+  // before any centre comes near; either proof skips the clamp, with the same bits.
+  float rho_lb = -INFINITY;
+  const float onorm = fabsf(o[0]) + fabsf(o[1]) + fabsf(o[2]);
+  // rho_lb after the ray moved from march distance t0 to t1 (|d| <= 1 + 1e-6; the fp32 rounding of
+  // both points p = o + d t, ~1.1e-7 (|o|_1 + 1.74 t) each, inside the absolute 1e-6 (1 + |o|_1 + t))
+  auto rho_moved = [&](float rl, float t0, float t1) {
+    return rl - (fabsf(t1 - t0) * 1.000001f + 1e-6f * (1.0f + onorm + fmaxf(t0, t1)));
+  };
+  auto all_safe = [&](float dist_lb, float rlb) {
+    return __all(dist_lb + rmin >= kSafeRho || rlb >= kSafeRho || gone) != 0;
+  };
   int split_par = 0;  // SPLIT: which of the two combine buffers the next step uses
 
   // every sweep visits all sphere pairs in one pass (records are not staged)
@@ -1860,12 +1895,14 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       // the loop so that D0 holds no register through the march.
       if (a.origin != nullptr && a.steps > 0 && !(SPLIT && a.cont_resume > 0)) {
         const float D0 = a.origin[view];
+        rho_lb = a.origin[RM_MAX_VIEWS_PER_CALL + view];  // at the eye
         if (__all((__float_as_uint(D0) & 0x7fffffffu) <= 0x7f800000u)) {
           const float p[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
           if (wave_escaped(0, p)) {
             dead = true;
           } else {  // == soft_min_march(p, all_safe(-inf) = false, inf) at p = o = the eye
             t = fminf(t + (gone ? gone_step : D0), kTMax);
+            rho_lb = rho_moved(rho_lb, 0.0f, t);
             lb = D0 - fabsf(D0);
             Dprev = D0;
             st0 = 1;
@@ -1894,8 +1931,9 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       cyc_t1 = cs[3 * R + li];
       cyc_t2 = cs[4 * R + li];
       gone = cs[5 * R + li] != 0.0f;
-      chist = __float_as_int(cs[6 * R + 2 * blk]);
-      steps_saved = __float_as_int(cs[6 * R + 2 * blk + 1]);
+      rho_lb = cs[6 * R + li];
+      chist = __float_as_int(cs[7 * R + 2 * blk]);
+      steps_saved = __float_as_int(cs[7 * R + 2 * blk + 1]);
       st0 = a.cont_resume;
     }
     for (int st = st0; !dead && st < a.steps; ++st) {
@@ -1909,9 +1947,10 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
           cs[3 * R + li] = cyc_t1;
           cs[4 * R + li] = cyc_t2;
           cs[5 * R + li] = gone ? 1.0f : 0.0f;
+          cs[6 * R + li] = rho_lb;
           if (lane == 0) {
-            cs[6 * R + 2 * blk] = __int_as_float(chist);
-            cs[6 * R + 2 * blk + 1] = __int_as_float(steps_saved);
+            cs[7 * R + 2 * blk] = __int_as_float(chist);
+            cs[7 * R + 2 * blk + 1] = __int_as_float(steps_saved);
             a.cont_list_w[atomicAdd(a.cont_count_w, 1)] = (int)blk;
           }
         }
@@ -1926,9 +1965,10 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
         break;
       }
       int choice;
-      const float D = soft_min_march(p, all_safe(lb), Dprev, choice);
+      const float D = soft_min_march(p, all_safe(lb, rho_lb), Dprev, choice);
       const float t_step = t;  // this step's state: (t_step, choice)
       t = fminf(t + (gone ? gone_step : D), kTMax);
+      rho_lb = rho_moved(rho_lb, t_step, t);
       // next point: hard min >= soft-min D here, moved by |D|
       lb = D - fabsf(D);
       Dprev = D;
@@ -1963,7 +2003,8 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
 #if RM_CYCLE_MAX >= 4
             else if (back == 3) t = cyc_t3;
 #endif
-            lb = (cf & 4) ? INFINITY : -INFINITY;  // all_safe(lb) of the final state = its bit 2
+            lb = (cf & 4) ? INFINITY : -INFINITY;  // all_safe(lb, rho_lb) of the final state = its bit 2
+            rho_lb = -INFINITY;
           } else {
             for (int k = st + 1; k < a.steps; ++k) {
               const float q[3] = {fmaf(d[0], t, o[0]) - c0x, fmaf(d[1], t, o[1]) - c0y, fmaf(d[2], t, o[2]) - c0z};
@@ -2026,7 +2067,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   float dmin = 0.0f, Zw = 1.0f, Zb = 1.0f, Df = 0.0f, mix[3] = {0.0f, 0.0f, 0.0f}, mu = 0.0f;
   if (!dead) {
     // ---- reconnect: t_final = t + sdf(p_approx) (renderer_diff.rs:30-39); renderer.rs has none
-    fast_a = all_safe(lb);
+    fast_a = all_safe(lb, rho_lb);
     if constexpr (MODE != kRender) {
       if constexpr (SPLIT) Da = soft_min_split(pa, fast_a, mA, sA);
       else Da = soft_min(pa, fast_a, mA, sA);
@@ -2036,7 +2077,8 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     p[1] = fmaf(d[1], tf, o[1]);
     p[2] = fmaf(d[2], tf, o[2]);
     // p_final is |Da| from p_approx; the taps another eps away
-    fast_f = MODE == kRender ? all_safe(lb - a.eps) : all_safe(-mA * inv_kappa - fabsf(Da) - a.eps);
+    fast_f = MODE == kRender ? all_safe(lb - a.eps, rho_lb - a.eps)
+                             : all_safe(-mA * inv_kappa - fabsf(Da) - a.eps, rho_moved(rho_lb, t, tf) - a.eps);
 
     // ---- detached normal (scene.rs:81-128): n = f / sqrt(|f|^2 + 1e-6) with f the central
     // differences (D(p + eps e_a) - D(p - eps e_a))_a; the 1e-6 keeps |n| ~ 0.2 at eps = 1e-4.
@@ -4114,7 +4156,7 @@ int run(rm_context* ctx, const Call& c) {
       int* counts[2] = {nullptr, nullptr};
       if (cont) {
         const long long rays = nb * kSplitRays;
-        const size_t need = (size_t)(6 * rays + 2 * nb) * sizeof(float) + (size_t)(2 * nb + 16) * sizeof(int);
+        const size_t need = (size_t)(7 * rays + 2 * nb) * sizeof(float) + (size_t)(2 * nb + 16) * sizeof(int);
         if (ctx->cont_bytes < need) {
           if (ctx->cont_buf) RM_HIP(ctx, hipFree(ctx->cont_buf));
           ctx->cont_buf = nullptr;
@@ -4122,7 +4164,7 @@ int run(rm_context* ctx, const Call& c) {
           RM_HIP(ctx, hipMalloc(&ctx->cont_buf, need));
           ctx->cont_bytes = need;
         }
-        lists[0] = reinterpret_cast<int*>(ctx->cont_buf + 6 * rays + 2 * nb);
+        lists[0] = reinterpret_cast<int*>(ctx->cont_buf + 7 * rays + 2 * nb);
         lists[1] = lists[0] + nb;
         counts[0] = lists[1] + nb;
         counts[1] = counts[0] + 1;

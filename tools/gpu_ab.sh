@@ -4,7 +4,7 @@
 # tools/build_variant.sh). Configs: m (metric, strong default), m10 (10 views per GPU), m16 (the default's
 # 80 views in calls of 16), ms / ms8 (the
 # default's calls on 4 streams, 16 / 8 views per call), c2, c2cj (C2 on the cameras.json poses), c3,
-# c4, c5, c5r1 (C5 on a fixed view), c5s (C5 on a 64x64 view), c5g (configs[4] on the grown model).
+# c4, c5, c5r1 (C5 on a fixed view), k5 (the metric at k = 5), c5s (C5 on a 64x64 view), c5g (configs[4] on the grown model).
 #   CONFIGS="m c5" ROUNDS=2 bash tools/gpu_ab.sh default "RM_X=1" lib:trace
 set -o pipefail
 mkdir -p gpurun_out/ab
@@ -24,6 +24,7 @@ for r in $(seq 1 $ROUNDS); do
     for c in $CONFIGS; do
       case $c in
         m) args="--steps 10" ;;
+        k5) args="--smooth-k 5 --steps 10" ;;
         m10) args="--views-per-gpu 10 --steps 20" ;;
         m16) args="--views-per-call 16 --steps 10" ;;
         ms) args="--streams 4 --steps 10" ;;
