@@ -65,7 +65,8 @@ def test_train_step_identical_with_early_exit(mods, monkeypatch, m, k, steps, si
         assert torch.equal(g0[key], g1[key]), key
     monkeypatch.setenv("RM_NO_EARLY_EXIT", "0")
     st = _stats(render, run)
-    assert st["waves"] == 2 * size * size // 64
+    # one count per 64-ray wave, or per split ray group (split march: 32 rays, RM_SPLIT_RAYS)
+    assert st["waves"] in (2 * size * size // 64, 2 * size * size // 32)
     if k == 32.0:
         assert st["waves_exited"] > 0 and st["steps_saved"] > 0
 

@@ -1,4 +1,4 @@
-"""Split march (RM_MARCH_SPLIT / env RM_SPLIT=1): 64 rays per block held by all four waves, each
+"""Split march (RM_MARCH_SPLIT / env RM_SPLIT=1): 32 rays per block (RM_SPLIT_RAYS) held by all four waves, each
 wave summing a quarter of the sphere row blocks per march step, the quarters added in wave order.
 
   * against the fp64 oracle (forward, backward, train step) at sphere counts whose row blocks
@@ -216,7 +216,7 @@ def test_split_continuation(rm, oracle, monkeypatch):
     _equal(base, _train(render, native, cams, W, H, tg, s, K, S, flags=native.RM_MARCH_NO_EARLY_EXIT))
     o, d = cam_rays(oracle, cams, W, H)
     check_fwd(base[2].reshape(-1, 3), oracle.render_diff(o.astype(np.float64), d.astype(np.float64), sc, S, K))
-    # the backward mode continues the same way (ragged: 3 views of 40x24 = 45 blocks of 64 rays)
+    # the backward mode continues the same way (ragged: 3 views of 40x24 = 90 blocks of 32 rays)
     import torch
     cams3 = model.ring_cameras(10, offset=5)[:3]
     g = torch.randn((3 * 40 * 24, 3), device="cuda", generator=torch.Generator("cuda").manual_seed(7))
