@@ -9,6 +9,8 @@ HIP path, per rank:
   all_reduce(grads) [N > 1]  (RCCL over xGMI; 7M+5 floats: gradient + loss)
   rm_optimizer_step          (activation chain rule + training.rs penalties + Burn Adam, which
                               also writes the activated parameters of the next step)
+On one GPU with one call per step the two calls are one (rm_train_step_camera_adam: for <= 64
+spheres the optimizer runs in the gradient reduction's last block; --fused-adam off: two calls).
 Views shard across ranks. Default: STRONG scaling -- a step covers --global-views 80 views of
 512x512 (a ring of 80 cameras) in all, split into contiguous parts over the N ranks (80 on one
 GPU, 10 per GPU on 8), so the total work per step is fixed as N grows; a rank issues its views in
@@ -116,6 +118,10 @@ def parse():
                     help="start from this scene.json (train.rs:238-262 layout, radius + 0.01 re-added as scene.rs:43) "
                          "instead of the synthetic seed-0 scene; --spheres is taken from the file (e.g. a model grown "
                          "by `rm_train train --split-scale 0 --split-move 0`, BASELINE configs[4])")
+    ap.add_argument("--fused-adam", choices=["on", "off"], default="on",
+                    help="on (one GPU, one call per step): the train step and the optimizer as ONE call "
+                         "(rm_train_step_camera_adam: for <= 64 spheres the optimizer runs in the gradient "
+                         "reduction's last block; bit-identical to the two calls)")
     ap.add_argument("--graph", choices=["on", "off"], default="off",
                     help="on (one GPU): capture one training step in a hipGraph (torch.cuda.CUDAGraph over the rm_* "
                          "calls, per-step scalars on the device: rm_bind_step_scalars) and replay it for the timed "
@@ -361,6 +367,10 @@ def main():
     # contiguous slice (no gather kernel, no host-built index tensor inside the timed loop)
     targets2 = torch.cat([targets, targets])
 
+    # one GPU, one call per step: the train step and the optimizer as one call (no gradient exchange
+    # between them)
+    fused_adam = args.fused_adam == "on" and world == 1 and slot_buf is None and ncalls == 1
+
     def step_fn(views, inv_count, grads_out, loss_out):
         # rm_train_step_camera over this rank's views (fused forward + loss seed + backward), in
         # calls of up to views_per_call views; the later calls add into the gradient and loss
@@ -376,6 +386,11 @@ def main():
             tg = targets2[part[0]:part[0] + len(part)]
             kw = dict(progress=min(progress["i"] / total_steps, 1.0), steps=S, inv_count=inv_count, march=march,
                       ctx=ctxs[c])
+            if fused_adam:  # the optimizer step in the same call (rm_train_step_camera_adam)
+                opt.train_step_camera([cams[j] for j in part], W, H, tg.view(-1, 3), K, kw["progress"], args.lr, S,
+                                      inv_count=inv_count, grads_packed=grads_out, loss=loss_out, march=march,
+                                      ctx=ctxs[c])
+                continue
             if slot_buf is None:  # one stream: the later calls add into the gradient and loss
                 rmr.train_step_camera([cams[j] for j in part], W, H, tg.view(-1, 3), model.scene(), K,
                                       grads_packed=grads_out, loss=loss_out, accumulate=c > 0, **kw)
@@ -392,7 +407,8 @@ def main():
             grads_out.copy_(tot[:nm])
             loss_out.copy_(tot[nm:])
 
-    dp = ViewShardedStep(shard, npix, rmm.packed_size(M), "cuda", step_fn, optim_fn=lambda g: opt.step(g, args.lr))
+    dp = ViewShardedStep(shard, npix, rmm.packed_size(M), "cuda", step_fn,
+                         optim_fn=None if fused_adam else (lambda g: opt.step(g, args.lr)))
     # graph mode: progress and Adam's step from a device record the optimizer advances (the
     # eager steps of the run read it too, so eager and replayed steps compute the same thing)
     sdev = None
@@ -668,7 +684,7 @@ def main():
                                    + (", fp16 colour / fp32 SDF" if args.color_dtype == "f16" else ""),
                        "width": W, "height": H, "spheres": M, "march_steps": S, "smooth_k": K,
                        "views_per_gpu": vpg, "global_views": shard.views_total, "views_per_call": views_per_call,
-                       "streams": nstreams, "graph": use_graph,
+                       "streams": nstreams, "graph": use_graph, "fused_adam": fused_adam,
                        "ring": ring, "ring_order": args.ring_order, "rays_per_step": rays_global, "radius_range": list(rr),
                        "color_storage": args.color_dtype, "sdf_dtype": "f32",
                        "cameras": args.cameras and os.path.relpath(os.path.abspath(args.cameras), ROOT),

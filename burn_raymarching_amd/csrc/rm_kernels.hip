@@ -2818,7 +2818,17 @@ struct FinalArgs {
   float *gc, *gcol, *gr, *gld, *gamb, *loss_sum;
   int accumulate;
   int* oturn;  // nullable: the cost-order turn word the reduction advances (KArgs::oturn)
+  // rm_train_step_camera_adam on a model of M <= kOptSmallMaxM spheres: the optimizer step on the
+  // packed gradient (grad = gc: the packed layout) runs in the reduction's last block
+  // (fused_optimizer); raw == nullptr otherwise
+  float *raw, *m1, *m2, *act_out, *loss_penalty;
+  _Float16* col_h;
+  rm_step_scalars* sdev;
+  unsigned* opt_arrival;  // the column blocks' arrival counter (zero between launches)
+  int step, with_pen;
+  float lr, wd;
 };
+__device__ void fused_optimizer(const FinalArgs& f, int M);
 
 #ifndef RM_REDUCE_BATCH
 #define RM_REDUCE_BATCH 8
@@ -2903,11 +2913,35 @@ __global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restric
   __syncthreads();
   finalize_block(S, (int)gridDim.y, M, Mpad, f, tot);
   if (tid == 0) __hip_atomic_store(arrivals + blockIdx.x * RM_RED_ARR_STRIDE, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (f.raw == nullptr) return;
+  // the optimizer step on the whole gradient, by the column block that finishes last: the same
+  // write-through hand-off one level up (finalize_block stored its gradient elements write-through)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(f.opt_arrival, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = prev == gridDim.x - 1 ? 1 : 0;
+  }
+  __syncthreads();
+  if (!last) return;
+  if (tid == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  fused_optimizer(f, M);
+  if (tid == 0) __hip_atomic_store(f.opt_arrival, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Pass 2 for the 256 columns of pass-1 column block blockIdx.x, by the block of that column block
 // that arrived last: thread t sums column t's kReduceSegs segments in the four chains s mod 4 of
 // rm_finalize_grads, combined (a0 + a1) + (a2 + a3) -- the same bits -- then the scatter.
+// a gradient element of the final scatter: write-through when the fused optimizer reads it
+__device__ __forceinline__ void put_grad(const FinalArgs& f, float* dst, float v) {
+  const float x = f.accumulate ? *dst + v : v;
+  if (f.raw != nullptr) __hip_atomic_store(dst, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else *dst = x;
+}
 __device__ void finalize_block(const float* S, int nseg, int M, int Mpad, const FinalArgs& f, float* tot) {
   const int ncols = Mpad * 8 + 8;
   const int tid = threadIdx.x;
@@ -2938,7 +2972,7 @@ __device__ void finalize_block(const float* S, int nseg, int M, int Mpad, const 
     const float v = tot[tid];
     float* dst = comp < 3 ? (f.gc ? f.gc + 3 * j + comp : nullptr)
                           : (comp == 3 ? (f.gr ? f.gr + j : nullptr) : (f.gcol ? f.gcol + 3 * j + (comp - 4) : nullptr));
-    if (dst) *dst = f.accumulate ? *dst + v : v;
+    if (dst) put_grad(f, dst, v);
     return;
   }
   const int sc = col - Mpad * 8;  // the scalars open their column block (Mpad * 8 % 256 == 0)
@@ -2952,10 +2986,10 @@ __device__ void finalize_block(const float* S, int nseg, int M, int Mpad, const 
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const float gv = (r[k] - ln[k] * proj) / len;
-      f.gld[k] = f.accumulate ? f.gld[k] + gv : gv;
+      put_grad(f, f.gld + k, gv);
     }
   } else if (sc == 3 && f.gamb) {
-    f.gamb[0] = f.accumulate ? f.gamb[0] + tot[tid] : tot[tid];
+    put_grad(f, f.gamb, tot[tid]);
   } else if (sc == 4 && f.loss_sum) {
     f.loss_sum[0] = f.accumulate ? f.loss_sum[0] + tot[tid] : tot[tid];
   }
@@ -3398,6 +3432,30 @@ __global__ __launch_bounds__(256) void rm_optimizer_small(float* __restrict__ ra
   }
 }
 
+// rm_optimizer_small's step inside the gradient reduction's last block (rm_reduce_partials,
+// FinalArgs::raw): the same functions on the same values -- the gradient read with agent-scope
+// loads after the hand-off -- so the same bits as the separate launch.
+__device__ void fused_optimizer(const FinalArgs& f, int M) {
+  const OptPrefetch pf = opt_prefetch(f.raw, f.m1, f.m2, M);
+  const int step = f.sdev != nullptr ? f.sdev->step : f.step;
+  const int n = 7 * M + 4, i0 = (int)threadIdx.x;
+  float g[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = i0 + 256 * h;
+    g[h] = i < n ? __hip_atomic_load(f.gc + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0f;
+  }
+  const OptPre o = opt_small_pre(pf, M, step, f.with_pen, f.loss_penalty);
+  opt_small_post(o, pf, g, f.raw, f.m1, f.m2, M, f.lr, f.wd, f.act_out, f.col_h);
+  if (f.sdev != nullptr) {  // every thread has read the step: the training step ends here
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      f.sdev->step += 1;
+      f.sdev->index += 1;
+    }
+  }
+}
+
 // The end of a training step with device step scalars bound (multi-block optimizer path).
 __global__ void rm_step_advance(rm_step_scalars* sdev) {
   if (threadIdx.x == 0) {
@@ -3443,6 +3501,8 @@ struct rm_context {
   std::vector<rm::CamBasis> cams_shadow;    // what the device table holds (the last upload)
   float* batch = nullptr;                   // rm_train_iteration's unfused path: the drawn batch (9 floats/ray)
   float* opt_pre = nullptr;                 // rm_train_iteration: the optimizer part of the launch's extra block
+  unsigned* opt_arrival = nullptr;          // rm_train_step_camera_adam: the reduction's column-block counter
+  bool adam_done = false;                   // the last call's optimizer ran inside its reduction
   size_t batch_bytes = 0;
   size_t rec_bytes = 0;
   long long stats_blocks = 0;               // ray blocks launched while stats are on
@@ -3658,11 +3718,20 @@ struct Call {
   // rm_train_iteration: org / dir / targets are the dataset arrays the kernel draws the batch
   // from, and the optimizer runs in the same launch (rm_small_kernel<kTrain, MB, true>)
   const SmallArgs* fused = nullptr;
+  // rm_train_step_camera_adam: the optimizer step on the packed gradient (grads->centers), run by
+  // the gradient reduction's last block where it can (rm_context::adam_done says whether it did)
+  struct Adam {
+    float *raw, *m1, *m2, *act_out, *loss_penalty;
+    _Float16* col_h;
+    int step, with_pen;
+    float lr, wd;
+  };
+  const Adam* adam = nullptr;
 };
 
 FinalArgs final_args(const Call& c, bool first) {
   const rm_grads* gp = c.grads;
-  FinalArgs fa;
+  FinalArgs fa{};
   fa.light_dir = c.scene->light_dir;
   fa.gc = gp->centers;
   fa.gcol = gp->colors;
@@ -3677,7 +3746,7 @@ FinalArgs final_args(const Call& c, bool first) {
 
 // The fixed-order cross-block reduction of a launch's nb partial records (a.partials) and the
 // gradient scatter into the caller's layout (rm_reduce_partials + rm_finalize_grads).
-int reduce_and_finalize(rm_context* ctx, const Call& c, const KArgs& a, long long nb, bool first) {
+int reduce_and_finalize(rm_context* ctx, const Call& c, const KArgs& a, long long nb, bool first, bool only = false) {
   FinalArgs fa = final_args(c, first);
   fa.oturn = const_cast<int*>(a.oturn);  // a keyed launch: its reduction advances the turn
   const int nblocks = (int)nb;
@@ -3694,6 +3763,28 @@ int reduce_and_finalize(rm_context* ctx, const Call& c, const KArgs& a, long lon
   if (fused && !ctx->red_arrivals) {
     RM_HIP(ctx, hipMalloc(&ctx->red_arrivals, sizeof(unsigned) * kRedArrivals));
     RM_HIP(ctx, hipMemsetAsync(ctx->red_arrivals, 0, sizeof(unsigned) * kRedArrivals, ctx->stream));
+  }
+  // rm_train_step_camera_adam: the optimizer in the reduction's last block (one launch, the only
+  // one of the call, M <= kOptSmallMaxM, the fused reduction)
+  if (c.adam != nullptr && only && fused && a.M <= kOptSmallMaxM && !env_is("RM_OPT_SMALL", '0') &&
+      !env_is("RM_FUSED_ADAM", '0')) {
+    if (!ctx->opt_arrival) {
+      RM_HIP(ctx, hipMalloc(&ctx->opt_arrival, 128));
+      RM_HIP(ctx, hipMemsetAsync(ctx->opt_arrival, 0, 128, ctx->stream));
+    }
+    fa.raw = c.adam->raw;
+    fa.m1 = c.adam->m1;
+    fa.m2 = c.adam->m2;
+    fa.act_out = c.adam->act_out;
+    fa.loss_penalty = c.adam->loss_penalty;
+    fa.col_h = c.adam->col_h;
+    fa.sdev = ctx->sdev;
+    fa.opt_arrival = ctx->opt_arrival;
+    fa.step = c.adam->step;
+    fa.with_pen = c.adam->with_pen;
+    fa.lr = c.adam->lr;
+    fa.wd = c.adam->wd;
+    ctx->adam_done = true;
   }
   hipLaunchKernelGGL(rm_reduce_partials, dim3((unsigned)xblocks, (unsigned)segs), dim3(256), 0, ctx->stream, a.partials,
                      a.rec, a.M, a.Mpad, nblocks, seg_len, S, fa, fused ? ctx->red_arrivals : nullptr);
@@ -4199,7 +4290,7 @@ int run(rm_context* ctx, const Call& c) {
         RM_HIP(ctx, hipGetLastError());
       }
     }
-    if (has_bwd && (rc = reduce_and_finalize(ctx, c, a, nb, first)) != RM_OK) return rc;
+    if (has_bwd && (rc = reduce_and_finalize(ctx, c, a, nb, first, first && nb == blocks_left)) != RM_OK) return rc;
     done += nr;
     first = false;
   } while (done < n);
@@ -4345,12 +4436,13 @@ void rm_destroy(rm_context* ctx) {
     if (ctx->ocnt) (void)hipFree(ctx->ocnt);
     if (ctx->rec) (void)hipFree(ctx->rec);
   }
-  if (ctx->arrivals || ctx->red_arrivals || ctx->batch || ctx->cams_dev || ctx->opt_pre) {
+  if (ctx->arrivals || ctx->red_arrivals || ctx->batch || ctx->cams_dev || ctx->opt_pre || ctx->opt_arrival) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->arrivals) (void)hipFree(ctx->arrivals);
     if (ctx->red_arrivals) (void)hipFree(ctx->red_arrivals);
     if (ctx->batch) (void)hipFree(ctx->batch);
     if (ctx->opt_pre) (void)hipFree(ctx->opt_pre);
+    if (ctx->opt_arrival) (void)hipFree(ctx->opt_arrival);
     if (ctx->cams_dev) (void)hipFree(ctx->cams_dev);
     if (ctx->cams_pin) (void)hipHostFree(ctx->cams_pin);
     for (hipEvent_t& e : ctx->cam_ev)
@@ -4684,6 +4776,54 @@ int rm_optimizer_step(rm_context* ctx, float* raw_packed, const float* grad_act_
                       int32_t with_penalties, float* loss_penalty, float* act_out) {
   return rm_optimizer_step_f16(ctx, raw_packed, grad_act_packed, adam_m, adam_v, num_spheres, step, lr, weight_decay,
                                with_penalties, loss_penalty, act_out, nullptr);
+}
+
+int rm_train_step_camera_adam(rm_context* ctx, const rm_camera* cams, int32_t num_views, int32_t width,
+                              int32_t height, const float* targets, float progress, float inv_count,
+                              const rm_march* march, float* act_packed, float* grad_packed, float* raw_packed,
+                              float* adam_m, float* adam_v, int32_t num_spheres, int32_t step, float lr,
+                              float weight_decay, int32_t with_penalties, float* loss_sum, float* loss_penalty,
+                              uint16_t* colors_f16_out) {
+  if (!ctx) return RM_ERR_INVALID_ARG;
+  if (!act_packed || !grad_packed || !raw_packed || !adam_m || !adam_v || !march)
+    return fail(ctx, RM_ERR_INVALID_ARG, "NULL model buffer");
+  if (num_spheres < 1 || num_spheres > RM_MAX_SPHERES) return fail(ctx, RM_ERR_INVALID_ARG, "bad num_spheres");
+  const bool f16 = (march->flags & RM_MARCH_COLOR_F16) != 0;
+  if (f16 != (colors_f16_out != nullptr))
+    return fail(ctx, RM_ERR_INVALID_ARG, "colors_f16_out goes with RM_MARCH_COLOR_F16 (and only with it)");
+  if (step < 1 && !ctx->sdev) return fail(ctx, RM_ERR_INVALID_ARG, "step counts from 1");
+  const int M = num_spheres;
+  rm_scene sc;
+  rm_scene_from_packed(act_packed, M, &sc);
+  if (f16) sc.colors = reinterpret_cast<const float*>(colors_f16_out);  // the fp16 colours the step renders
+  rm_grads gr;
+  rm_grads_from_packed(grad_packed, M, &gr);
+  Call c;
+  c.mode = kTrain;
+  c.cam = true;
+  c.cams = cams;
+  c.views = num_views;
+  c.W = width;
+  c.H = height;
+  c.targets = targets;
+  c.progress = progress;
+  c.inv_count = inv_count;
+  c.scene = &sc;
+  c.march = march;
+  c.grads = &gr;
+  c.loss_sum = loss_sum;
+  c.accumulate = 0;
+  const Call::Adam ad{raw_packed, adam_m, adam_v, act_packed, loss_penalty, reinterpret_cast<_Float16*>(colors_f16_out),
+                      step, with_penalties ? 1 : 0, lr, weight_decay};
+  c.adam = &ad;
+  ctx->adam_done = false;
+  int rc = run(ctx, c);
+  const bool done = ctx->adam_done;
+  ctx->adam_done = false;
+  if (rc != RM_OK || done) return rc;
+  // not fused (more than 64 spheres, the small-scene kernel, sub-launches): the optimizer call
+  return rm_optimizer_step_f16(ctx, raw_packed, grad_packed, adam_m, adam_v, M, step, lr, weight_decay,
+                               with_penalties, loss_penalty, act_packed, colors_f16_out);
 }
 
 int rm_train_iteration(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,

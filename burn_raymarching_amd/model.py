@@ -136,6 +136,43 @@ class Adam:
         self.model._act_valid = True
 
 
+    def train_step_camera(self, cams, width, height, targets, smooth_k, progress, lr, steps=40, *, inv_count=None,
+                          grads_packed=None, loss=None, penalty_out=None, march=None, ctx=None):
+        """rm_train_step_camera_adam: the camera-mode train step of this optimizer's model into
+        grads_packed / loss (overwritten), then this optimizer's step on it -- one call; for up to
+        64 spheres the optimizer runs inside the gradient reduction. The same results bit for bit
+        as render.train_step_camera followed by step()."""
+        from . import render as R
+        mdl = self.model
+        cams = list(cams)
+        if not 1 <= len(cams) <= native.RM_MAX_VIEWS_PER_CALL:
+            raise ValueError(f"1..{native.RM_MAX_VIEWS_PER_CALL} views per call")
+        n = len(cams) * width * height
+        targets = R._f32(targets, (n, 3), "targets")
+        if inv_count is None:
+            inv_count = 1.0 / (3.0 * n)
+        dev = mdl.raw.device
+        if grads_packed is None:
+            grads_packed = torch.zeros(packed_size(mdl.num_spheres), device=dev)
+        if loss is None:
+            loss = torch.zeros((1,), device=dev)
+        if ctx is None:
+            ctx = context(dev)
+        sc = mdl.scene()  # the activated parameters (and fp16 colours) are current
+        if march is None:
+            march = native.march_params(steps, smooth_k)
+        march = sc.march_for(march)
+        self.t += 1
+        p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+        ctx.check(ctx._lib.rm_train_step_camera_adam(
+            ctx.handle, native.cameras(cams), len(cams), width, height, p(targets), float(progress), float(inv_count),
+            ctypes.byref(march), p(mdl._act), p(grads_packed), p(mdl.raw), p(self.m), p(self.v), mdl.num_spheres,
+            self.t, float(lr), float(self.weight_decay), 1 if self.with_penalties else 0, p(loss), p(penalty_out),
+            p(mdl._col_h)), "rm_train_step_camera_adam")
+        mdl._act_valid = True
+        return loss, grads_packed
+
+
 # ---- seeded synthetic scenes (BASELINE.md "Synthetic inputs") ------------------------------
 def synthetic_scene(num_spheres: int, seed: int = 0, radius_range=(0.03, 0.12)) -> dict:
     """numpy PCG64 default_rng(seed): centers uniform in the ball of radius 0.6, activated radii

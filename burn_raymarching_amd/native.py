@@ -100,6 +100,9 @@ SIGNATURES = {
     "rm_grads_from_packed": (None, [_P, _I32, ctypes.POINTER(RmGrads)]),
     "rm_optimizer_step": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _F, _F, _I32, _P, _P]),
     "rm_optimizer_step_f16": (ctypes.c_int, [_P, _P, _P, _P, _P, _I32, _I32, _F, _F, _I32, _P, _P, _P]),
+    "rm_train_step_camera_adam": (ctypes.c_int, [_P, ctypes.POINTER(RmCamera), _I32, _I32, _I32, _P, _F, _F,
+                                                  ctypes.POINTER(RmMarch), _P, _P, _P, _P, _P, _I32, _I32, _F, _F,
+                                                  _I32, _P, _P, _P]),
     "rm_train_iteration": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _I64, _I64, ctypes.c_uint64,
                                           ctypes.c_uint64, ctypes.c_uint64, _F, _F, ctypes.POINTER(RmMarch), _P, _P,
                                           _P, _P, _P, _I32, _I32, _F, _F, _I32, _P, _P]),

@@ -117,11 +117,11 @@ typedef struct rm_march {
  * the colour blend, the SDF, the march and every gradient stay fp32 (grads->colors is fp32,
  * the master gradient). See rm_optimizer_step_f16 for the optimizer side. */
 #define RM_MARCH_COLOR_F16 256
-/* Split march: a ray block takes 64 rays (one 8x8 pixel quadrant in camera mode) held by all
+/* Split march: a ray block takes 32 rays (half an 8x8 pixel quadrant in camera mode) held by all
  * four waves of the block; every march step each wave sums a quarter of the spheres on the
  * matrix cores and the quarters are added in a fixed order, so the waves march in lockstep;
- * the post-march sweeps are split the same way and each wave seeds the backward of a quarter of
- * the rays. A ray that marches every step then spreads over four SIMDs: for launches that fill
+ * the post-march sweeps are split the same way, and the backward shares the sphere groups out
+ * over the four waves. A ray that marches every step then spreads over four SIMDs: for launches that fill
  * the GPU a few times (BASELINE configs[4]), where a few rays march all steps while the rest
  * leave early. Taken automatically from 256 spheres for launches of at most 262,144 rays and
  * from 512 spheres for at most 1,048,576 rays; this flag forces it, RM_MARCH_NO_SPLIT forbids
@@ -331,6 +331,29 @@ int rm_optimizer_step(rm_context* ctx, float* raw_packed, const float* grad_act_
 int rm_optimizer_step_f16(rm_context* ctx, float* raw_packed, const float* grad_act_packed, float* adam_m,
                           float* adam_v, int32_t num_spheres, int32_t step, float lr, float weight_decay,
                           int32_t with_penalties, float* loss_penalty, float* act_out, uint16_t* colors_f16_out);
+
+/* One single-process training step on whole views (train.rs:182-198: model.forward, compute_loss,
+ * loss.backward(), optim.step), replacing rm_train_step_camera -> rm_optimizer_step[_f16] with the
+ * same arguments and the same results bit for bit:
+ *   1. the render of act_packed (activated packed parameters; with RM_MARCH_COLOR_F16 in
+ *      march->flags the colours come from colors_f16_out), the loss seed and the backward into
+ *      grad_packed ((7M+4) floats, overwritten) and loss_sum (1 float, overwritten), as
+ *      rm_train_step_camera with progress and inv_count;
+ *   2. the optimizer step on raw_packed / adam_m / adam_v (step, lr, weight_decay,
+ *      with_penalties, loss_penalty nullable) writing the updated activated parameters to
+ *      act_packed (and, fp16-colour models, their rounded colours to colors_f16_out), as
+ *      rm_optimizer_step_f16 with act_out = act_packed.
+ * Models of up to 64 spheres run the optimizer inside the call's gradient reduction, in the block
+ * that completes the gradient (env RM_FUSED_ADAM=0 turns this off): one launch fewer per step.
+ * Otherwise -- more spheres, the small-scene kernel, more than one ray sub-launch -- the two calls
+ * run as such. Bound step scalars (rm_bind_step_scalars) apply as to the two calls. Not for
+ * data-parallel training: the gradient is consumed before it could be all-reduced. */
+int rm_train_step_camera_adam(rm_context* ctx, const rm_camera* cams, int32_t num_views, int32_t width,
+                              int32_t height, const float* targets, float progress, float inv_count,
+                              const rm_march* march, float* act_packed, float* grad_packed, float* raw_packed,
+                              float* adam_m, float* adam_v, int32_t num_spheres, int32_t step, float lr,
+                              float weight_decay, int32_t with_penalties, float* loss_sum, float* loss_penalty,
+                              uint16_t* colors_f16_out);
 
 /* One step of the reference training loop (train.rs:169-198) for one process, replacing the
  * sequence rm_sample_batch -> rm_train_step -> rm_optimizer_step with the same arguments and

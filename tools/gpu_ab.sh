@@ -1,7 +1,7 @@
 # Same-box A/B of variants on bench configurations, alternating A B A B over ROUNDS rounds.
 # A variant is "default", an environment assignment list ("RM_SPLIT=0 RM_SMALL=1") or
 # "lib:<name>" (the kernel library burn_raymarching_amd/lib/var/<name>.so, built with
-# tools/build_variant.sh). Configs: m (metric, strong default), m10 (10 views per GPU), m16 (the default's
+# tools/build_variant.sh) or "args:<bench.py arguments>" (e.g. "args:--fused-adam off"). Configs: m (metric, strong default), m10 (10 views per GPU), m16 (the default's
 # 80 views in calls of 16), ms / ms8 (the
 # default's calls on 4 streams, 16 / 8 views per call), c2, c2cj (C2 on the cameras.json poses), c3,
 # c4, c5, c5r1 (C5 on a fixed view), k5 (the metric at k = 5), c5s (C5 on a 64x64 view), c5g (configs[4] on the grown model).
@@ -16,9 +16,11 @@ for r in $(seq 1 $ROUNDS); do
     i=$((i + 1))
     unset RM_LIB_PATH
     envs=""
+    extra=""
     case $v in
       default) ;;
       lib:*) export RM_LIB_PATH=burn_raymarching_amd/lib/var/${v#lib:}.so ;;
+      args:*) extra=${v#args:} ;;
       *) envs=$v ;;
     esac
     for c in $CONFIGS; do
@@ -38,7 +40,7 @@ for r in $(seq 1 $ROUNDS); do
         c5s) args="--width 64 --height 64 --spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 4 --warmup 2" ;;
         c5g) args="--march-steps 128 --views-per-gpu 1 --steps 6 --warmup 2 --color-dtype f16 --cameras tests/golden/cameras.json --targets dango --scene-json profiles/r05a_grown_scene_4096.json" ;;
       esac
-      env $envs timeout -k 10 200 python bench.py --cpu-baseline off $args > gpurun_out/ab/${c}_v${i}_$r.json \
+      env $envs timeout -k 10 200 python bench.py --cpu-baseline off $args $extra > gpurun_out/ab/${c}_v${i}_$r.json \
         2> gpurun_out/ab/${c}_v${i}_$r.err || { tail -5 gpurun_out/ab/${c}_v${i}_$r.err; exit 1; }
       # a variant whose executed work differs from the first variant's did other work (e.g. trained
       # differently): its time is not comparable, and the line says so
