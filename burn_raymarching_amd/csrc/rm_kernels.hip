@@ -1756,7 +1756,10 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     choice = (none ? 1 : 0) | (fixed ? 2 : 0) | (fast ? 4 : 0);
     if ((none || fixed) && a.mfma) {
       const float k2 = kappa * kappa;
-      const int nrb = a.Mpad / 16;
+      // opaque per step: the row-block count's derived guards are formed here, not hoisted out
+      // of the march loop as long-lived lane masks (SGPR pressure: spills to v_writelane)
+      int nrb = a.Mpad / 16;
+      asm volatile("" : "+s"(nrb));
       uint4* xa = reinterpret_cast<uint4*>(L.slots) + wave * 64;
       uint4* xb = reinterpret_cast<uint4*>(L.slots) + kWaves * 64 + wave * 64;
       float* xs = L.slots + kWaves * 64 * 8 + wave * 64;
@@ -2936,6 +2939,18 @@ __global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restric
 // Pass 2 for the 256 columns of pass-1 column block blockIdx.x, by the block of that column block
 // that arrived last: thread t sums column t's kReduceSegs segments in the four chains s mod 4 of
 // rm_finalize_grads, combined (a0 + a1) + (a2 + a3) -- the same bits -- then the scatter.
+// The light-direction gradient (renderer_diff.rs:49-50, the Jacobian of ld / |ld|) of the summed
+// per-ray terms r: component k of (r - ldn (ldn . r)) / |ld|. One function with contraction off for
+// both pass-2 forms (finalize_block, rm_finalize_grads), so that they give the same bits.
+__device__ __forceinline__ float light_grad(const float (&r)[3], const float* light_dir, int k) {
+#pragma clang fp contract(off)
+  const float l0 = light_dir[0], l1 = light_dir[1], l2 = light_dir[2];
+  const float len = sqrtf(l0 * l0 + l1 * l1 + l2 * l2);
+  const float ln[3] = {l0 / len, l1 / len, l2 / len};
+  const float proj = ln[0] * r[0] + ln[1] * r[1] + ln[2] * r[2];
+  return (r[k] - ln[k] * proj) / len;
+}
+
 // a gradient element of the final scatter: write-through when the fused optimizer reads it
 __device__ __forceinline__ void put_grad(const FinalArgs& f, float* dst, float v) {
   const float x = f.accumulate ? *dst + v : v;
@@ -2977,17 +2992,9 @@ __device__ void finalize_block(const float* S, int nseg, int M, int Mpad, const 
   }
   const int sc = col - Mpad * 8;  // the scalars open their column block (Mpad * 8 % 256 == 0)
   if (sc == 0 && f.gld) {
-    const float r0 = tot[tid], r1 = tot[tid + 1], r2 = tot[tid + 2];
-    const float l0 = f.light_dir[0], l1 = f.light_dir[1], l2 = f.light_dir[2];
-    const float len = sqrtf(l0 * l0 + l1 * l1 + l2 * l2);
-    const float ln[3] = {l0 / len, l1 / len, l2 / len};
-    const float r[3] = {r0, r1, r2};
-    const float proj = ln[0] * r0 + ln[1] * r1 + ln[2] * r2;
+    const float r[3] = {tot[tid], tot[tid + 1], tot[tid + 2]};
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-      const float gv = (r[k] - ln[k] * proj) / len;
-      put_grad(f, f.gld + k, gv);
-    }
+    for (int k = 0; k < 3; ++k) put_grad(f, f.gld + k, light_grad(r, f.light_dir, k));
   } else if (sc == 3 && f.gamb) {
     put_grad(f, f.gamb, tot[tid]);
   } else if (sc == 4 && f.loss_sum) {
@@ -3039,15 +3046,10 @@ __global__ __launch_bounds__(256) void rm_finalize_grads(const float* __restrict
   }
   const int sc = col - Mpad * 8;  // Mpad * 8 is a multiple of 64: the scalars open their block
   if (sc == 0 && f.gld) {
-    const float r0 = seg_sum(cl), r1 = seg_sum(cl + 1), r2 = seg_sum(cl + 2);
-    const float l0 = f.light_dir[0], l1 = f.light_dir[1], l2 = f.light_dir[2];
-    const float len = sqrtf(l0 * l0 + l1 * l1 + l2 * l2);
-    const float ln[3] = {l0 / len, l1 / len, l2 / len};
-    const float r[3] = {r0, r1, r2};
-    const float proj = ln[0] * r0 + ln[1] * r1 + ln[2] * r2;
+    const float r[3] = {seg_sum(cl), seg_sum(cl + 1), seg_sum(cl + 2)};
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
-      const float gv = (r[c] - ln[c] * proj) / len;
+      const float gv = light_grad(r, f.light_dir, c);
       f.gld[c] = f.accumulate ? f.gld[c] + gv : gv;
     }
   } else if (sc == 3 && f.gamb) {
