@@ -9,8 +9,8 @@ HIP path, per rank:
   all_reduce(grads) [N > 1]  (RCCL over xGMI; 7M+5 floats: gradient + loss)
   rm_optimizer_step          (activation chain rule + training.rs penalties + Burn Adam, which
                               also writes the activated parameters of the next step)
-On one GPU with one call per step the two calls are one (rm_train_step_camera_adam: for <= 64
-spheres the optimizer runs in the gradient reduction's last block; --fused-adam off: two calls).
+With --fused-adam on (one GPU, one call per step) the two calls are one (rm_train_step_camera_adam:
+for <= 64 spheres the optimizer runs in the gradient reduction's last block).
 Views shard across ranks. Default: STRONG scaling -- a step covers --global-views 80 views of
 512x512 (a ring of 80 cameras) in all, split into contiguous parts over the N ranks (80 on one
 GPU, 10 per GPU on 8), so the total work per step is fixed as N grows; a rank issues its views in
@@ -118,10 +118,11 @@ def parse():
                     help="start from this scene.json (train.rs:238-262 layout, radius + 0.01 re-added as scene.rs:43) "
                          "instead of the synthetic seed-0 scene; --spheres is taken from the file (e.g. a model grown "
                          "by `rm_train train --split-scale 0 --split-move 0`, BASELINE configs[4])")
-    ap.add_argument("--fused-adam", choices=["on", "off"], default="on",
+    ap.add_argument("--fused-adam", choices=["on", "off"], default="off",
                     help="on (one GPU, one call per step): the train step and the optimizer as ONE call "
                          "(rm_train_step_camera_adam: for <= 64 spheres the optimizer runs in the gradient "
-                         "reduction's last block; bit-identical to the two calls)")
+                         "reduction's last block; bit-identical to the two calls). Off by default: no measured "
+                         "gain at C2 (profiles/r06_ab.txt)")
     ap.add_argument("--graph", choices=["on", "off"], default="off",
                     help="on (one GPU): capture one training step in a hipGraph (torch.cuda.CUDAGraph over the rm_* "
                          "calls, per-step scalars on the device: rm_bind_step_scalars) and replay it for the timed "
