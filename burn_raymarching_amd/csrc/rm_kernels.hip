@@ -136,6 +136,7 @@ static_assert(kSplitWaves == 2 || kSplitWaves == 4, "split blocks have 2 or 4 wa
 constexpr int kSplitRays = RM_SPLIT_RAYS;
 static_assert(kSplitRays == 64 || kSplitRays == 32 || kSplitRays == 16, "split blocks hold 64, 32 or 16 rays");
 constexpr int kSplitCB = kSplitRays / 16;  // column blocks of 16 rays in the split march's tiles
+constexpr int kContClasses = 4;  // classes of the split continuation's block lists
 constexpr long long kSplitMaxRays = 262144;
 #ifndef RM_REDUCE_SEGS
 #define RM_REDUCE_SEGS 128
@@ -205,7 +206,10 @@ struct KArgs {
   // Continuation of a split launch (split_cont_steps, see run()): with cont_cap > 0 a block whose
   // rays still march at step cont_cap saves its march state, appends its logical block to
   // cont_list_w and ends; a launch with cont_resume = that step runs the saved blocks
-  // (cont_list[0..*cont_count)) from there (and may defer again at its own cont_cap).
+  // (cont_list[0..*cont_count)) from there (and may defer again at its own cont_cap). The lists
+  // are kContClasses class lists of cont_stride entries each, with kContClasses counts: a deferred
+  // block goes to the class of its rays still moving (the most first), and a continuation launch
+  // runs the classes in order -- the blocks likely to march to the end start first.
   // cont_state: [7][cont_rays] per ray (t, lb, D_prev, t one and two steps back, gone, rho_lb) then
   // [blocks][2] per block (choice history, steps saved).
   int cont_cap, cont_resume;
@@ -214,6 +218,8 @@ struct KArgs {
   const int* cont_count;
   int* cont_list_w;
   int* cont_count_w;
+  int cont_stride;   // entries per class list
+  int cont_order;    // 0: every deferred block in class 0 (arrival order)
   long long cont_rays;
 #ifdef RM_BLOCK_TRACE
   unsigned long long* btrace;  // measurement build: per-wave timing records (rm_ray_kernel)
@@ -1594,8 +1600,15 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   int cls = -1;  // the block's cost class in the previous launch (cost-ordered dispatch), else -1
   long long blk;
   if (SPLIT && a.cont_resume > 0) {  // continuation launch: the blocks the first launch deferred
-    if ((int)blockIdx.x >= *a.cont_count) return;
-    blk = a.cont_list[blockIdx.x];
+    // position blockIdx.x of the class-major concatenation of the class lists
+    int b = (int)blockIdx.x, c = 0;
+    for (; c < kContClasses; ++c) {
+      const int n = a.cont_count[c];
+      if (b < n) break;
+      b -= n;
+    }
+    if (c == kContClasses) return;
+    blk = a.cont_list[(long long)c * a.cont_stride + b];
   } else {
     blk = ray_block(a, &cls);
   }
@@ -1941,6 +1954,12 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     }
     for (int st = st0; !dead && st < a.steps; ++st) {
       if (SPLIT && a.cont_cap > 0 && st == a.cont_cap) {  // defer: save the state at the top of this step
+        // the block's class: how many of its rays still move (the last step longer than 1e-4 of
+        // max(t, 1)); converged and gone rays leave the march soon (cycle exit, escape)
+        const int moving = __popcll(__ballot(lane < kSplitRays && valid && !gone &&
+                                             fabsf(Dprev) > 1e-4f * fmaxf(t, 1.0f)));
+        const int cls = !a.cont_order ? 0
+                        : (moving >= kSplitRays / 4 ? 0 : (moving >= kSplitRays / 10 + 1 ? 1 : (moving > 0 ? 2 : 3)));
         if (wave == 0 && lane < kSplitRays) {  // the four waves (and a ray's copies) hold the same state
           float* cs = a.cont_state;
           const long long R = a.cont_rays;
@@ -1954,7 +1973,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
           if (lane == 0) {
             cs[7 * R + 2 * blk] = __int_as_float(chist);
             cs[7 * R + 2 * blk + 1] = __int_as_float(steps_saved);
-            a.cont_list_w[atomicAdd(a.cont_count_w, 1)] = (int)blk;
+            a.cont_list_w[(long long)cls * a.cont_stride + atomicAdd(a.cont_count_w + cls, 1)] = (int)blk;
           }
         }
         return;
@@ -4249,7 +4268,8 @@ int run(rm_context* ctx, const Call& c) {
       int* counts[2] = {nullptr, nullptr};
       if (cont) {
         const long long rays = nb * kSplitRays;
-        const size_t need = (size_t)(7 * rays + 2 * nb) * sizeof(float) + (size_t)(2 * nb + 16) * sizeof(int);
+        const size_t need = (size_t)(7 * rays + 2 * nb) * sizeof(float) +
+                            (size_t)(2 * kContClasses * nb + 2 * kContClasses + 16) * sizeof(int);
         if (ctx->cont_bytes < need) {
           if (ctx->cont_buf) RM_HIP(ctx, hipFree(ctx->cont_buf));
           ctx->cont_buf = nullptr;
@@ -4258,16 +4278,18 @@ int run(rm_context* ctx, const Call& c) {
           ctx->cont_bytes = need;
         }
         lists[0] = reinterpret_cast<int*>(ctx->cont_buf + 7 * rays + 2 * nb);
-        lists[1] = lists[0] + nb;
-        counts[0] = lists[1] + nb;
-        counts[1] = counts[0] + 1;
+        lists[1] = lists[0] + kContClasses * nb;
+        counts[0] = lists[1] + kContClasses * nb;
+        counts[1] = counts[0] + kContClasses;
         a.cont_state = ctx->cont_buf;
         a.cont_rays = rays;
         a.cont_list_w = lists[0];
         a.cont_count_w = counts[0];
         a.cont_cap = caps[0];
         a.cont_resume = 0;
-        RM_HIP(ctx, hipMemsetAsync(counts[0], 0, 2 * sizeof(int), ctx->stream));
+        a.cont_stride = (int)nb;
+        a.cont_order = env_is("RM_CONT_ORDER", '0') ? 0 : 1;
+        RM_HIP(ctx, hipMemsetAsync(counts[0], 0, 2 * kContClasses * sizeof(int), ctx->stream));
       }
       if (c.mode == kFwd) launch_ray<kFwd>(c.cam, split, grid, lds, ctx->stream, a, ev0, ev1);
       else if (c.mode == kBwd) launch_ray<kBwd>(c.cam, split, grid, lds, ctx->stream, a, ev0, ev1);
