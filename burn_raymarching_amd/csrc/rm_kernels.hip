@@ -1954,12 +1954,21 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     }
     for (int st = st0; !dead && st < a.steps; ++st) {
       if (SPLIT && a.cont_cap > 0 && st == a.cont_cap) {  // defer: save the state at the top of this step
-        // the block's class: how many of its rays still move (the last step longer than 1e-4 of
-        // max(t, 1)); converged and gone rays leave the march soon (cycle exit, escape)
-        const int moving = __popcll(__ballot(lane < kSplitRays && valid && !gone &&
-                                             fabsf(Dprev) > 1e-4f * fmaxf(t, 1.0f)));
-        const int cls = !a.cont_order ? 0
-                        : (moving >= kSplitRays / 4 ? 0 : (moving >= kSplitRays / 10 + 1 ? 1 : (moving > 0 ? 2 : 3)));
+        // the block's class: the march steps its slowest ray still needs, predicted from its last
+        // two steps as a linear convergence (the next step ~ rho times the last; grazing rays have
+        // rho near 1) down to a few ulp of t, where the cycle exit takes it; gone rays need none
+        float need = 0.0f;
+        if (lane < kSplitRays && valid && !gone) {
+          const float d1 = fabsf(t - cyc_t1), d0 = fabsf(cyc_t1 - cyc_t2);
+          const float tiny = 4.0f * fmaxf(fabsf(t), 1e-3f) * 1.2e-7f;
+          if (d1 > tiny) {
+            const float rho = d0 > 0.0f ? d1 / d0 : 1.0f;
+            need = (rho >= 0.97f || !(rho == rho)) ? 1e9f : flog2(d1 / tiny) / -flog2(rho);
+          }
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) need = fmaxf(need, __shfl_xor(need, off));
+        const int cls = !a.cont_order ? 0 : (need >= 60.0f ? 0 : (need >= 30.0f ? 1 : (need >= 10.0f ? 2 : 3)));
         if (wave == 0 && lane < kSplitRays) {  // the four waves (and a ray's copies) hold the same state
           float* cs = a.cont_state;
           const long long R = a.cont_rays;
