@@ -14,7 +14,12 @@ against it:
     value(N) = 80 * 512 * 512 / T(N) Mrays/s
 
     python tools/predict_scaling.py --bench profiles/r05_bench.json --balance profiles/r04b_shard_balance.json \
-        --allreduce profiles/r05b_allreduce.json [--hop-us 2.5] > profiles/r05_scaling_prediction.json
+        --allreduce profiles/r05b_allreduce.json [--hop-us 2.5] [--slices 2=... 4=... 8=...] \
+        > profiles/r05_scaling_prediction.json
+With --slices the N-rank step is one rank's step measured on one GPU (bench.py --global-views
+80/N --ring 80: the rank's views in one launch with its own record, origin, reduction and
+optimizer kernels), its kernel stretched by the balance study's slowest-over-mean rank (the
+one-GPU run rotates through the ring, so it times the mean rank), plus the modelled all-reduce.
 """
 import argparse
 import json
@@ -26,6 +31,10 @@ def main():
     ap.add_argument("--balance", required=True, help="tools/shard_balance.py output")
     ap.add_argument("--allreduce", required=True, help="tools/allreduce_probe.py output")
     ap.add_argument("--order", default="spread")
+    ap.add_argument("--slices", nargs="*", default=[],
+                    help="N=file pairs (e.g. 8=profiles/r06i_slice_10.json): bench lines of one rank's step at N "
+                         "ranks measured on one GPU (bench.py --global-views 80/N --ring 80); where given, T(N) uses "
+                         "the measured step (its train kernel and its own small kernels) instead of the scaled slice")
     ap.add_argument("--hop-us", type=float, default=2.5,
                     help="modelled latency of one xGMI ring hop of a few-KB message (no measurement on a "
                          "one-GPU box; an assumption, stated in the output)")
@@ -42,7 +51,26 @@ def main():
                       "kernel_ms_n1": kern1, "outside_ms": round(outside, 4), "allreduce_floor_us": floor_us,
                       "hop_us_assumed": args.hop_us},
            "curve": {}}
+    measured = {}
+    for pair in args.slices:
+        n, f = pair.split("=", 1)
+        measured[int(n)] = json.load(open(f))
+    out["inputs"]["slices"] = {str(n): f for n, f in (p.split("=", 1) for p in args.slices)}
     for n in (1, 2, 4, 8):
+        if n in measured:  # one rank's whole step measured on one GPU, plus the all-reduce
+            m = measured[n]
+            # the one-GPU run rotates through the ring, so it times the mean rank's slice; the step
+            # waits for the slowest rank: the balance study's max / mean of the N slices adds that
+            sl = bal[str(n)]["slice_ms"]
+            imb = max(sl) / (sum(sl) / len(sl))
+            kern = m["roofline"]["kernel_ms_per_step"]
+            ar_ms = (floor_us + 2 * (n - 1) * args.hop_us) * 1e-3
+            t = m["ms_per_step"] + kern * (imb - 1) + ar_ms
+            out["curve"][str(n)] = {"step_ms": round(t, 4), "train_kernel_ms": round(kern * imb, 4),
+                                    "slice_step_ms_measured": m["ms_per_step"], "slice_kernel_ms_measured": kern,
+                                    "slowest_over_mean_rank": round(imb, 4), "allreduce_ms": round(ar_ms, 4),
+                                    "mrays_s": round(rays / (t * 1e-3) / 1e6, 1)}
+            continue
         slice_ms = kern1 if n == 1 else max(bal[str(n)]["slice_ms"])
         # the balance study timed each rank's slice as its own launch (as the rank runs it), on a
         # scene earlier in training than the bench's timed steps: its slices are scaled by the
