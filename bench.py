@@ -37,9 +37,10 @@ Extra objects on the JSON line:
                    algorithmic FLOP = 16*(S+10)*M per ray. `achieved`/`frac`
                    count the sweeps that ran (executed_frac, from the kernel's work counters in an
                    untimed replay of the timed steps from a snapshot of the training state:
-                   waves whose rays all escaped stop early, and the normal is one sweep instead of
-                   six); `canonical` is the full 16*(S+10)*M per ray over the kernel time of a
-                   second replay with the early exit off; `pmc` quotes the committed rocprofv3 SQ summary
+                   waves whose rays all escaped stop early, the normal is one sweep instead of
+                   six, and the two backward sweeps run only for rays with non-zero seeds);
+                   `canonical` is the work of a second replay with the early exit off (every ray's
+                   S+3 sweeps, the seeded rays' backward sweeps) over its kernel time; `pmc` quotes the committed rocprofv3 SQ summary
                    (profiles/r*_pmc_sq.json) for this workload; traffic = HBM bytes per launch from
                    the committed FETCH_SIZE / WRITE_SIZE summary (profiles/r*_pmc_traffic.json).
   cpu_baseline  -- the oracle's fp32 reference-order C restatement (OpenMP) on a bounded strided
@@ -82,6 +83,10 @@ def parse():
     ap.add_argument("--spheres", type=int, default=256)
     ap.add_argument("--march-steps", type=int, default=32)
     ap.add_argument("--smooth-k", type=float, default=32.0)
+    ap.add_argument("--anneal-k", type=float, default=None, metavar="K0",
+                    help="anneal the soft-min sharpness as train.rs:174 does (k = K0 + (K - K0) * progress), "
+                         "over the timed steps: the warmup runs at K0, timed step j of K at "
+                         "K0 + (K - K0) * j / (K - 1)")
     ap.add_argument("--global-views", type=int, default=None,
                     help="strong scaling (the default, %d views): views per step over ALL ranks, split into "
                          "contiguous parts over the ranks" % DEFAULT_GLOBAL_VIEWS)
@@ -329,6 +334,8 @@ def main():
         ring = max(args.ring, shard.views_total)
         cams = [rmm.ring_cameras(ring)[a] for a in ring_order(ring, args.ring_order)]
     shard.ring = ring
+    if use_graph and args.anneal_k is not None:
+        raise SystemExit("--graph on freezes the march parameters of the captured step: no --anneal-k")
     if use_graph and shard.views_total != ring:
         # a captured step freezes its views, target slice and camera bases: replays would train the
         # captured views while eager steps rotate through the ring -- not the same run
@@ -422,6 +429,9 @@ def main():
 
     def step(i):
         progress["i"] = i
+        if args.anneal_k is not None:  # train.rs:174 over the timed steps
+            f = min(max((i - args.warmup) / max(args.steps - 1, 1), 0.0), 1.0)
+            march.smooth_k = float(args.anneal_k + (K - args.anneal_k) * f)
         dp(i)
         if i == 0 and args.dump_grad and not grad0:
             grad0.append(dp.buf.detach().clone())
@@ -585,7 +595,14 @@ def main():
     # takes the normal's six central-difference sweeps as one gradient sweep)
     sweeps_total = waves_total * (S + 10)
     waves_post = max(waves_total - blocks_skipped * 4 - st["waves_exited"], 0)
-    sweeps_run = (waves_total - blocks_skipped * 4) * S - st["steps_saved"] + waves_post * 5
+    # the two backward sweeps run only for the rays with non-zero seeds (the kernel's counters;
+    # in wave units: rays per counted wave, 64, or a split block's rays)
+    rays_replayed = rays_per_rank * args.steps
+    rays_per_wave = rays_replayed / waves_total
+    seeded = st.get("seeded_rays", 0) + st.get("seeded_rays_a", 0)
+    bwd_counted = seeded > 0 or waves_post == 0  # (the small kernel, M <= 32, does not count them)
+    bwd_sweeps = seeded / rays_per_wave if bwd_counted else waves_post * 2
+    sweeps_run = (waves_total - blocks_skipped * 4) * S - st["steps_saved"] + waves_post * 3 + bwd_sweeps
     have_stats = st["waves"] > 0  # --aux-steps 0 (PMC passes): no statistics, no executed-work figure
     executed_frac = max(0.0, sweeps_run / sweeps_total) if have_stats else None
     kern_step_ms = kern_step_ms or float("nan")  # no timed launches (--kernel-timing off)
@@ -616,14 +633,22 @@ def main():
         # with the exit off every ray runs S march + 5 post-march sweeps (reconnect, shade, the normal
         # as the one gradient sweep the kernel runs, 2 backward): 16*(S+5)*M FLOP; the reference's
         # 16*(S+10)*M credits its six normal taps, which this kernel does not run
-        ach = FLOP_PER_EVAL * (S + 5) * M * rays_per_rank / (canon_ms * 1e-3) / 1e12
+        # the backward sweeps of the seeded rays only (the same rays with the exit on and off)
+        bwd_per_step = (seeded / args.steps) if (bwd_counted and have_stats) else 2 * rays_per_rank
+        flop_canon = FLOP_PER_EVAL * M * ((S + 3) * rays_per_rank + bwd_per_step)
+        ach = flop_canon / (canon_ms * 1e-3) / 1e12
+        ach_all = FLOP_PER_EVAL * (S + 5) * M * rays_per_rank / (canon_ms * 1e-3) / 1e12
         ach_ref = flop_per_ray * rays_per_rank / (canon_ms * 1e-3) / 1e12
         canonical = {"kernel_ms": round(canon_ms, 4), "achieved": round(ach, 3),
-                     "frac": round(ach / PEAK_FP32_TFLOPS, 4), "flop_per_ray": FLOP_PER_EVAL * (S + 5) * M,
+                     "frac": round(ach / PEAK_FP32_TFLOPS, 4),
+                     "flop_per_ray": round(flop_canon / rays_per_rank),
+                     "frac_backward_all_rays": round(ach_all / PEAK_FP32_TFLOPS, 4),
                      "frac_reference_taps": round(ach_ref / PEAK_FP32_TFLOPS, 4),
-                     "note": "exit off: 16*(S+5)*M FLOP per ray (the sweeps the kernel runs) over the kernel time of "
-                             "the timed steps replayed untimed with the early exit off; frac_reference_taps credits "
-                             "the reference's 16*(S+10)*M (six normal taps)"}
+                     "note": "exit off: 16*M*(S+3) FLOP per ray (march, reconnect, normal, shade) + 16*M per backward "
+                             "sweep of a ray with non-zero seeds (rm_stats seeded_rays + seeded_rays_a) over the kernel "
+                             "time of the timed steps replayed untimed with the early exit off; "
+                             "frac_backward_all_rays credits both backward sweeps to every ray (16*(S+5)*M), "
+                             "frac_reference_taps the reference's 16*(S+10)*M (six normal taps)"}
     roofline = None if launches == 0 else {
         "bound": "valu",
         "kernel": "rm_ray_kernel<train,camera>",
@@ -646,6 +671,11 @@ def main():
         "rays_per_launch": rays_per_rank,
         "executed_frac": round(executed_frac, 4) if have_stats else None,
         "executed_frac_source": "rm_stats counters, untimed replay of the timed steps",
+        "backward_rays_frac": (None if not (have_stats and bwd_counted) else
+                               [round(st.get("seeded_rays", 0) / rays_replayed, 4),
+                                round(st.get("seeded_rays_a", 0) / rays_replayed, 4)]),
+        "backward_rays_note": "fraction of the rays the two backward sweeps ran for (non-zero seeds; the "
+                              "others contribute exact zeros and are not swept): counted as executed work",
         "achieved_all_rays": round(flop_per_ray * rays_per_rank / (kern_step_ms * 1e-3) / 1e12, 3),
         "canonical": canonical,
         "pmc": None if pmc is None else dict(pmc, source=pmc_src),
@@ -681,9 +711,11 @@ def main():
                      f", targets {args.targets}, poses {'cameras.json' if args.cameras else 'synthetic ring'}"),
             "config": {"workload": (f"train step fwd+bwd, {shard.views_total} {W}x{H} views per step over all GPUs"
                                     if strong else f"train step fwd+bwd, {vpg} {W}x{H} view(s) per GPU")
-                                   + f", {M} spheres, {S} march steps, k={K:g}, camera mode, Adam"
+                                   + f", {M} spheres, {S} march steps, "
+                                   + (f"k={K:g}" if args.anneal_k is None else f"k annealed {args.anneal_k:g}->{K:g}")
+                                   + ", camera mode, Adam"
                                    + (", fp16 colour / fp32 SDF" if args.color_dtype == "f16" else ""),
-                       "width": W, "height": H, "spheres": M, "march_steps": S, "smooth_k": K,
+                       "width": W, "height": H, "spheres": M, "march_steps": S, "smooth_k": K, "anneal_k_from": args.anneal_k,
                        "views_per_gpu": vpg, "global_views": shard.views_total, "views_per_call": views_per_call,
                        "streams": nstreams, "graph": use_graph, "fused_adam": fused_adam,
                        "ring": ring, "ring_order": args.ring_order, "rays_per_step": rays_global, "radius_range": list(rr),

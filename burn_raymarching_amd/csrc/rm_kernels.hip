@@ -49,6 +49,9 @@
 #ifndef RM_BWD_TRANSPOSED
 #define RM_BWD_TRANSPOSED 1  // backward sweeps with one sphere per lane (0: one ray per lane)
 #endif
+#ifndef RM_BWD_PSQ_REG
+#define RM_BWD_PSQ_REG 0  // backward sweeps form |p|^2 from p in registers (1) or read it from LDS (0)
+#endif
 #ifndef RM_MARCH_SCHED
 #define RM_MARCH_SCHED 1  // scheduling barriers in the matrix-core march loop (0: compiler's order)
 #endif
@@ -154,7 +157,9 @@ struct KArgs {
   int cull;    // skip blocks whose rays provably escape the scene (RM_MARCH_SKIP_ESCAPED)
   float cull_min_d;  // scene distance at which the silhouette mask is exactly 0
   float lse_slack;  // ln(M) / k (rounded up): the hard min exceeds the soft-min by at most this
-  unsigned long long* stats;  // nullable: [0] += 1 per escaped (skipped) block
+  unsigned long long* stats;  // nullable: [0] += 1 per escaped (skipped) block, [1] exited waves,
+                              // [2] march steps saved, [3] RM_LANE_STATS, [4] / [5] rays the two
+                              // backward sweeps run for (non-zero seeds)
   float gone_d;               // > 0: rays that provably escape past this distance are `gone` (see the march)
   int early_exit;             // waves whose rays are all gone stop marching
   int split;                  // split march (RM_MARCH_SPLIT): 64 rays per block, a quarter of the spheres per wave
@@ -265,6 +270,7 @@ __host__ __device__ inline size_t tiles_offset(int npairs, int nprep) {
 }
 // Then the escape thresholds of the march: kEscTab floats (see write_bound).
 constexpr int kEscTab = 64;
+constexpr int kStatsWords = 6;  // rm_stats device counters (KArgs::stats)
 __host__ __device__ inline size_t esc_offset(int npairs, int nprep) {
   const size_t nrb = (size_t)npairs / 8;
   return tiles_offset(npairs, nprep) + nrb * 64 * 16 + nrb * 32 * sizeof(float);
@@ -504,7 +510,10 @@ __device__ void write_bound(const KArgs& a, float* hdr, float* esc) {
       // four dependent instructions per step (v_sqrt_f32: 1 ulp, inside the round-up)
       const float two_c2 = 2.0f * inv_shrink * inv_shrink * (1.0f + 1e-6f), nrp2 = -rp * rp,
                   half_up = 0.5f * (1.0f + 1e-5f);
-      for (int n = 1; n <= (int)threadIdx.x; ++n) T = fmaf(rp + fsqrt(fmaf(two_c2 * T, T, nrp2)), half_up, 1e-6f);
+      // the march reads T(n) for n <= a.steps only: entries past it repeat T(a.steps) (>= T(n)),
+      // which shortens the longest dependent chain at S < kEscTab
+      const int nmax = min((int)threadIdx.x, a.steps);
+      for (int n = 1; n <= nmax; ++n) T = fmaf(rp + fsqrt(fmaf(two_c2 * T, T, nrp2)), half_up, 1e-6f);
       tv = T * (1.0f + 1e-6f);
     }
     esc[threadIdx.x] = tv;
@@ -2476,6 +2485,9 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       }
     }
     if (lane == 0) nsrc[wave] = n1;
+    // work statistics: the rays the backward sweeps run for (a split block's rays are wave 0's)
+    if (a.stats != nullptr && lane == 0 && n1 > 0 && (!SPLIT || wave == 0))
+      atomicAdd(a.stats + 4, (unsigned long long)n1);
 #pragma unroll
     for (int sw = 0; sw < kWv; ++sw) gta[(wave * kWaves + sw) * 64 + lane] = 0.0f;
     __syncthreads();  // every live wave's image and count
@@ -2529,7 +2541,12 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
                   continue;
                 }
                 const int s0 = 2 * (b + uu);
-                const f2 PX = pair(sw, 0, s0), PY = pair(sw, 1, s0), PZ = pair(sw, 2, s0), PP = pair(sw, 3, s0);
+                const f2 PX = pair(sw, 0, s0), PY = pair(sw, 1, s0), PZ = pair(sw, 2, s0);
+#if RM_BWD_PSQ_REG
+                const f2 PP = fma2(PZ, PZ, fma2(PY, PY, PX * PX));  // == psq(p), lane by lane
+#else
+                const f2 PP = pair(sw, 3, s0);
+#endif
                 const f2 DM = pair(sw, 4, s0), IZ = pair(sw, 5, s0), BS = pair(sw, 6, s0), MG = pair(sw, 7, s0);
                 const f2 G0 = pair(sw, 8, s0), G1 = pair(sw, 9, s0), G2 = pair(sw, 10, s0);
                 const f2 DX = pair(sw, 11, s0), DY = pair(sw, 12, s0), DZ = pair(sw, 13, s0);
@@ -2627,6 +2644,8 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       }
     }
     if (lane == 0) nsrc[wave] = n2;
+    if (a.stats != nullptr && lane == 0 && n2 > 0 && (!SPLIT || wave == 0))
+      atomicAdd(a.stats + 5, (unsigned long long)n2);
     __syncthreads();  // every live wave's sweep-2 image and count
     const int srcs2 = sources();
     const int nsw2 = __popc(srcs2);
@@ -2664,7 +2683,12 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
             const int nps = (nsrc[sw] + 1) >> 1;
             for (int i2 = 0; i2 < nps; ++i2) {
               const int s0 = 2 * i2;
-              const f2 PX = pair(sw, 0, s0), PY = pair(sw, 1, s0), PZ = pair(sw, 2, s0), PP = pair(sw, 3, s0);
+              const f2 PX = pair(sw, 0, s0), PY = pair(sw, 1, s0), PZ = pair(sw, 2, s0);
+#if RM_BWD_PSQ_REG
+              const f2 PP = fma2(PZ, PZ, fma2(PY, PY, PX * PX));  // == psq(pa), lane by lane
+#else
+              const f2 PP = pair(sw, 3, s0);
+#endif
               const f2 MA = pair(sw, 4, s0), HS = pair(sw, 5, s0);
               f2 q = fma2(PZ, GZ, fma2(PY, GY, fma2(PX, GX, PP + CC)));  // == qpair: the reconnect sweep's q
               const f2 qraw = q;
@@ -3519,7 +3543,7 @@ struct rm_context {
   bool timing = false;  // record hipEvents around every per-ray kernel launch
   std::vector<std::pair<hipEvent_t, hipEvent_t>> events;
   size_t events_used = 0;
-  unsigned long long* stats_dev = nullptr;  // escaped-block counter (rm_stats_enable)
+  unsigned long long* stats_dev = nullptr;  // work counters (rm_stats_enable), kStatsWords words
   int* esc_flags = nullptr;                 // per-block escape flags, kMaxBlocksPerLaunch ints
   void* rec = nullptr;                      // sphere records of the current call (rm_prep_kernel)
   unsigned* arrivals = nullptr;             // rm_small_kernel's arrival counter (zero between launches)
@@ -4423,8 +4447,8 @@ int rm_debug_block_trace(rm_context* ctx, unsigned long long* host, int64_t cap_
 int rm_stats_enable(rm_context* ctx, int32_t enable) {
   if (!ctx) return RM_ERR_INVALID_ARG;
   if (enable && !ctx->stats_dev) {
-    RM_HIP(ctx, hipMalloc(&ctx->stats_dev, 4 * sizeof(unsigned long long)));
-    RM_HIP(ctx, hipMemsetAsync(ctx->stats_dev, 0, 4 * sizeof(unsigned long long), ctx->stream));
+    RM_HIP(ctx, hipMalloc(&ctx->stats_dev, kStatsWords * sizeof(unsigned long long)));
+    RM_HIP(ctx, hipMemsetAsync(ctx->stats_dev, 0, kStatsWords * sizeof(unsigned long long), ctx->stream));
     ctx->stats_blocks = 0;
     ctx->stats_waves = 0;
   } else if (!enable && ctx->stats_dev) {
@@ -4438,7 +4462,7 @@ int rm_stats_enable(rm_context* ctx, int32_t enable) {
 int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset) {
   if (!ctx || !out) return RM_ERR_INVALID_ARG;
   if (!ctx->stats_dev) return fail(ctx, RM_ERR_INVALID_ARG, "stats are not enabled");
-  unsigned long long v[4];
+  unsigned long long v[kStatsWords];
   RM_HIP(ctx, hipMemcpyAsync(v, ctx->stats_dev, sizeof v, hipMemcpyDeviceToHost, ctx->stream));
   RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
   out->blocks = ctx->stats_blocks;
@@ -4446,6 +4470,8 @@ int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset) {
   out->waves = ctx->stats_waves;
   out->waves_exited = (int64_t)v[1];
   out->steps_saved = (int64_t)v[2];
+  out->seeded_rays = (int64_t)v[4];
+  out->seeded_rays_a = (int64_t)v[5];
 #ifdef RM_LANE_STATS
   std::fprintf(stderr, "RM_LANE_STATS escaped_lane_sweeps %llu\n", v[3]);
 #endif

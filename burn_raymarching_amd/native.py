@@ -48,7 +48,7 @@ RM_MARCH_NO_SPLIT = 1024
 
 class RmStats(ctypes.Structure):
     _fields_ = [("blocks", _I64), ("blocks_skipped", _I64), ("waves", _I64), ("waves_exited", _I64),
-                ("steps_saved", _I64)]
+                ("steps_saved", _I64), ("seeded_rays", _I64), ("seeded_rays_a", _I64)]
 
 
 class RmCamera(ctypes.Structure):
@@ -184,7 +184,8 @@ class Context:
         self.check(self._lib.rm_stats_enable(self.handle, 1 if enable else 0), "rm_stats_enable")
 
     def collect_stats(self, reset: bool = True) -> dict:
-        """rm_stats since the last reset: blocks, blocks_skipped, waves, waves_exited, steps_saved."""
+        """rm_stats since the last reset: blocks, blocks_skipped, waves, waves_exited, steps_saved,
+        seeded_rays, seeded_rays_a."""
         st = RmStats()
         self.check(self._lib.rm_stats_collect(self.handle, ctypes.byref(st), 1 if reset else 0), "rm_stats_collect")
         return {name: getattr(st, name) for name, _ in RmStats._fields_}

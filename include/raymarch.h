@@ -289,7 +289,10 @@ int rm_timing_collect(rm_context* ctx, double* total_ms, int64_t* launches, int3
 /* ---- work statistics -------------------------------------------------------- */
 /* rm_stats_enable(ctx, 1): count, for every later per-ray launch, the ray blocks (256 rays)
  * launched, those skipped whole by RM_MARCH_SKIP_ESCAPED, and the waves (64 rays) that left
- * the march early because all their rays escaped, with the march steps they saved.
+ * the march early because all their rays escaped, with the march steps they saved, and the rays
+ * the backward modes' two gradient sweeps ran for (the rays with non-zero seeds: a ray whose
+ * seeds are 0 contributes exact zeros and is not swept; the general kernel counts them, the
+ * small kernel (M <= 32) reports 0).
  * rm_stats_collect synchronises the stream; reset != 0 clears the counters. */
 typedef struct rm_stats {
   int64_t blocks;          /* ray blocks launched */
@@ -297,6 +300,8 @@ typedef struct rm_stats {
   int64_t waves;           /* waves launched (4 per block) */
   int64_t waves_exited;    /* waves that stopped marching early (all rays escaped) */
   int64_t steps_saved;     /* march steps those waves did not run */
+  int64_t seeded_rays;     /* rays the first backward sweep (at p) ran for */
+  int64_t seeded_rays_a;   /* rays the second backward sweep (at p_approx) ran for */
 } rm_stats;
 int rm_stats_enable(rm_context* ctx, int32_t enable);
 int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset);

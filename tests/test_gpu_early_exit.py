@@ -69,6 +69,13 @@ def test_train_step_identical_with_early_exit(mods, monkeypatch, m, k, steps, si
     assert st["waves"] in (2 * size * size // 64, 2 * size * size // 32)
     if k == 32.0:
         assert st["waves_exited"] > 0 and st["steps_saved"] > 0
+    # the backward sweeps' ray counts (rays with non-zero seeds): the same rays with the exit off,
+    # the second sweep's a subset of the first's
+    rays = 2 * size * size
+    assert 0 < st["seeded_rays_a"] <= st["seeded_rays"] <= rays
+    monkeypatch.setenv("RM_NO_EARLY_EXIT", "1")
+    st_off = _stats(render, run)
+    assert (st_off["seeded_rays"], st_off["seeded_rays_a"]) == (st["seeded_rays"], st["seeded_rays_a"])
 
 
 def test_forward_backward_and_render_identical(mods, monkeypatch):
