@@ -686,6 +686,25 @@ __device__ __forceinline__ f2 qpair(const f2& PX, const f2& PY, const f2& PZ, co
 }
 __device__ __forceinline__ float psq(const float p[3]) { return fmaf(p[2], p[2], fmaf(p[1], p[1], p[0] * p[0])); }
 
+// A wave's 64 spheres' 8 record columns (lane = sphere, v[7] = 0) stored as two contiguous 1 KB
+// runs: store h covers spheres 32 h .. 32 h + 31, lane l writing half (l & 1) of sphere
+// 32 h + (l >> 1) (two half-line stores per lane would touch every line twice). Every lane of
+// the wave calls it; nsph = the group's spheres below Mpad.
+__device__ __forceinline__ void store_group_cols(float* rec_grp, const float (&v)[8], int lane, int nsph) {
+  const int s = lane >> 1, hf = lane & 1;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    float o[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float lo = __shfl(v[c], 32 * h + s), hi = __shfl(v[4 + c], 32 * h + s);
+      o[c] = hf ? hi : lo;
+    }
+    const int sph = 32 * h + s;
+    if (sph < nsph) reinterpret_cast<float4*>(rec_grp)[2 * sph + hf] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // ---- forward sweeps -----------------------------------------------------------------
 // Base-2 log-sum-exp of v_j = kappa*(r_j - rho_j) over a tile (sdf.rs:36-40), running max m and
 // shifted sum s carried across tiles; chunks of 16 spheres, one rescale exp per chunk.
@@ -2363,6 +2382,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   // waves; an odd count is padded with a copy of the last ray whose seeds are zero (exact zero
   // terms). Distances are formed with the same fp32 operations and operands as the forward sweeps
   // (qpair, delta_pair_rsq), so dd = dmin - delta <= 0 and v - mA <= 0 hold exactly.
+  bool any_seed = true;  // block-uniform: some ray of the block has a non-zero seed
   {
     (void)slots;
     (void)live_sum;
@@ -2452,12 +2472,11 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
           if (c < nst) acc[c] += part[c * 64 + lane];
       }
       const int j = gl * 64 + lane;
-      if (j < a.Mpad) {
+      if (ncomp == 8) {
+        store_group_cols(rec + (long long)gl * 64 * 8, acc, lane, min(64, a.Mpad - gl * 64));
+      } else if (j < a.Mpad) {
         float4* dst = reinterpret_cast<float4*>(rec + (long long)j * 8);
-        if (ncomp == 8) {
-          dst[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-          dst[1] = make_float4(acc[4], acc[5], acc[6], 0.0f);
-        } else {
+        {
           float4 v = dst[0];
           v.x += acc[0];
           v.y += acc[1];
@@ -2586,11 +2605,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
           const float v[8] = {agc[0].x + agc[0].y, agc[1].x + agc[1].y, agc[2].x + agc[2].y, agr.x + agr.y,
                               acol[0].x + acol[0].y, acol[1].x + acol[1].y, acol[2].x + acol[2].y, 0.0f};
           if (kb == 0 && ke == nsw1) {  // every source: the group's columns, written by this wave alone
-            if (j < a.Mpad) {
-              float4* dst = reinterpret_cast<float4*>(rec + (long long)j * 8);
-              dst[0] = make_float4(v[0], v[1], v[2], v[3]);
-              dst[1] = make_float4(v[4], v[5], v[6], 0.0f);
-            }
+            store_group_cols(rec + (long long)grp * 64 * 8, v, lane, min(64, a.Mpad - grp * 64));
           } else if (grp == u0 / nsw1) {
 #pragma unroll
             for (int c = 0; c < 8; ++c) p0[c] = v[c];
@@ -2600,13 +2615,8 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
           }
         }
       };
-      if (nsw1 == 0) {  // no ray of the block has a seed: the group columns are zeros
-        for (int grp = arank; grp < ngrp; grp += __popc(alive))
-          if (grp * 64 + lane < a.Mpad) {
-            float4* dst = reinterpret_cast<float4*>(rec + (long long)(grp * 64 + lane) * 8);
-            dst[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            dst[1] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-          }
+      if (nsw1 == 0) {  // no ray of the block has a seed: its columns are zeros, not written (live flag 0)
+        any_seed = false;
       } else if (fast_f) {
         sweep1(std::false_type{});
       } else {
@@ -2851,7 +2861,12 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     float acc = wscal[lane];
 #pragma unroll
     for (int w = 1; w < (SPLIT ? kSplitWaves : kWaves); ++w) acc += wscal[w * 8 + lane];
-    rec[(long long)a.Mpad * 8 + lane] = lane == 7 ? 1.0f : acc;  // scalar 7: live flag
+#if RM_BWD_TRANSPOSED
+    const float live = any_seed ? 1.0f : 0.0f;
+#else
+    const float live = 1.0f;
+#endif
+    rec[(long long)a.Mpad * 8 + lane] = lane == 7 ? live : acc;  // scalar 7: live flag
   }
 }
 
@@ -2859,8 +2874,9 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
 // Partial record of one ray block (rec = Mpad*8 + 8 floats):
 //   [Mpad][8] (gc.xyz, gr, gcol.rgb, 0) -- backward sweep 1's terms, sweep 2's (gc, gr) terms added
 //   by the block itself -- | 8 scalars
-// Scalar 7 is the block's live flag: 0 when every wave of the block left the march early (its
-// per-sphere columns are all zero and were not written), 1 otherwise.
+// Scalar 7 is the block's live flag: 0 when every wave of the block left the march early or no ray
+// of it has a non-zero backward seed (its per-sphere columns are all zero and were not written),
+// 1 otherwise.
 // Output columns (ncols = Mpad*8 + 8): [Mpad][8] combined per-sphere grads | 8 scalars.
 //
 // Pass 1, grid (column blocks x segments of ray blocks): each block sums its segment for its 256

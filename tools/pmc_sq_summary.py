@@ -18,7 +18,8 @@ Derived, per launch of rm_ray_kernel<2, true>:
     the full per-ray work that ran, measured by the hardware, to compare with the bench's
     stats-based executed_frac / executed_frac(exit off) of the same steps (bench.json: a bench
     line with the PMC passes' arguments and the replays on; exit off runs S - 1 march steps (the
-    shared origin step) and 5 post-march sweeps of the S + 10 per wave).
+    shared origin step), 3 post-march sweeps and the seeded rays' 2 backward sweeps of the S + 10
+    per wave).
 """
 import csv
 import glob
@@ -102,7 +103,11 @@ def main():
         S = bench["config"]["march_steps"]
         ef = bench["roofline"]["executed_frac"]
         res["executed_frac_stats"] = ef
-        res["executed_ratio_stats"] = ef / ((S - 1 + 5) / (S + 10))
+        # exit off: S - 1 march steps (the shared origin step), 3 post-march sweeps, and the two
+        # backward sweeps of the rays with non-zero seeds (the same rays with the exit on and off)
+        bw = bench["roofline"].get("backward_rays_frac")
+        post = 3 + sum(bw) if bw else 5
+        res["executed_ratio_stats"] = ef / ((S - 1 + post) / (S + 10))
         res["stats_source"] = os.path.basename(sys.argv[6])
     data = json.load(open(out)) if os.path.exists(out) else {}
     data.setdefault("train_kernel", {})[key] = res
