@@ -609,7 +609,8 @@ def main():
     achieved_tf = (flop_per_ray * rays_per_rank * executed_frac / (kern_step_ms * 1e-3) / 1e12
                    if have_stats else None)
     key = (f"{W}x{H}_M{M}_S{S}_V{vpg}" + ("_c16" if args.color_dtype == "f16" else "")
-           + (f"_k{K:g}" if K != 32.0 else "") + ("_cj" if args.cameras else "")
+           + (f"_k{K:g}" if K != 32.0 else "") + (f"_ka{args.anneal_k:g}" if args.anneal_k is not None else "")
+           + ("_cj" if args.cameras else "")
            + ("_grown" if args.scene_json else ""))
     # per step (the step's launches together), like `achieved`; per launch where no per-step
     # summary exists for this workload

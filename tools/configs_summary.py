@@ -29,6 +29,7 @@ def main():
                  "ms_per_step": d["ms_per_step"], "ms_per_step_median": d.get("ms_per_step_median"),
                  "train_kernel_ms": r.get("kernel_ms_per_step"), "frac": r.get("frac"),
                  "executed_frac": r.get("executed_frac"), "canonical_frac": (r.get("canonical") or {}).get("frac"),
+                 "backward_rays_frac": r.get("backward_rays_frac"), "value_exit_off": d.get("value_exit_off"),
                  "finite": d.get("finite")}
         if r.get("kernel_ms_per_step") is not None:  # the step's wall time outside the train kernel
             entry["outside_us_per_step"] = round((d["ms_per_step"] - r["kernel_ms_per_step"]) * 1e3, 2)

@@ -7,6 +7,7 @@
 #   C4 1024x1024 / 1024 / 64 steps, 4 views (the per-GPU share of 32 views on 8 GPUs)
 #   C4s the same 32 views on one GPU (strong-scaling N = 1 leg)
 #   C5 512x512 / 4096 / 128 steps, 1 view (fp32 and fp16 colour)     k5: the metric at k = 5
+#   ka: the metric with k annealed 5 -> 32 over the timed steps (train.rs:174)
 #   C2cj / C3cj: C2 / C3 on the data/cameras.json poses (C2 on the reference's own target PNGs)
 #   C5g: configs[4] on a model GROWN to 4096 spheres by prune_and_split (see grow below)
 #   bash tools/gpu_configs.sh <tag> [names...]   (CALIB=<fetch_calibration.json>: calibrated traffic)
@@ -64,5 +65,6 @@ run C4s 1024x1024_M1024_S64_V32 --width 1024 --height 1024 --spheres 1024 --marc
 run C5 512x512_M4096_S128_V1 --spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 6 --warmup 2 && \
 run C5f16 512x512_M4096_S128_V1_c16 --spheres 4096 --march-steps 128 --views-per-gpu 1 --steps 6 --warmup 2 --color-dtype f16 && \
 run k5 512x512_M256_S32_V80_k5 --smooth-k 5 --steps 10 && \
+run ka 512x512_M256_S32_V80_ka5 --anneal-k 5 --steps 10 && \
 python3 tools/configs_summary.py $O profiles/${TAG}_configs.json && cp profiles/${TAG}_configs.json $O/ && \
 { [ -z "$PMC" ] || cp profiles/${TAG}_pmc_traffic.json profiles/${TAG}_pmc_sq.json $O/; }
