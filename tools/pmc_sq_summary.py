@@ -9,7 +9,8 @@ SQ_WAVES over `bench.py --aux-steps 0` with the early exit on (default) and off
 SQ_ACTIVE_INST_VALU on the default run. Each directory also holds the kernel trace of its run
 (durations). SQ instruction counters count wave-instructions (one per wave64 instruction).
 
-Derived, per launch of rm_ray_kernel<2, true>:
+Derived, per train step (the dispatches of rm_ray_kernel<2, true> and of a split launch's
+continuation kernel rm_cont_kernel<2, true> summed; steps = the first kernel's dispatches):
   * trans_issue_frac: transcendental wave-instructions x their measured issue cost (cycles per
     wave-instruction per SIMD, profiles/r01_valu_rates.txt: sqrt 8.35, exp 9.37, log 8.37,
     rcp 8.44, rsq 8.26 -> 8.6 on the kernel's mix) / (1024 SIMDs x clock x kernel time) -- the
@@ -47,18 +48,25 @@ def rows(path, suffix):
 
 
 def counters(path):
-    vals = {}
+    """Per train step: the counters summed over the step's train dispatches (a split launch with a
+    continuation dispatches twice per step), divided by the steps (the first kernel's dispatches)."""
+    vals, firsts = {}, {}
     for r in rows(path, "counter_collection.csv"):
         if not is_train(r["Kernel_Name"]):
             continue
-        vals.setdefault(r["Counter_Name"], []).append(float(r["Counter_Value"]))
-    return {k: sum(v) / len(v) for k, v in vals.items()}, max((len(v) for v in vals.values()), default=0)
+        vals[r["Counter_Name"]] = vals.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+        if KERNEL in r["Kernel_Name"]:
+            firsts.setdefault(r["Counter_Name"], set()).add(r["Dispatch_Id"])
+    steps = max((len(v) for v in firsts.values()), default=0)
+    return {k: v / steps for k, v in vals.items()} if steps else {}, steps
 
 
 def duration_ns(path):
-    d = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows(path, "kernel_trace.csv")
-         if is_train(r["Kernel_Name"])]
-    return sum(d) / len(d) if d else None
+    """Per train step: the summed durations of the step's train dispatches."""
+    tr = [r for r in rows(path, "kernel_trace.csv") if is_train(r["Kernel_Name"])]
+    steps = sum(1 for r in tr if KERNEL in r["Kernel_Name"])
+    d = sum(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in tr)
+    return d / steps if steps else None
 
 
 def main():
