@@ -132,6 +132,10 @@ def parse():
                     help="on (one GPU): capture one training step in a hipGraph (torch.cuda.CUDAGraph over the rm_* "
                          "calls, per-step scalars on the device: rm_bind_step_scalars) and replay it for the timed "
                          "steps; the train-kernel time then comes from the statistics replay (eager, timed)")
+    ap.add_argument("--as-rank", default=None, metavar="R/N",
+                    help="one GPU runs rank R's share of an N-rank strong-scaling step alone: its fixed views of "
+                         "the global ones, the global ray count, no all-reduce (what that rank's GPU does per step "
+                         "at N ranks, for tools/predict_scaling.py); value = this rank's rays per second")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--kernel-timing", choices=["on", "off"], default="on",
@@ -154,6 +158,14 @@ def parse():
         args.ring_order = "spread" if args.global_views is not None else "contiguous"
     if args.global_views is not None and args.global_views < args.gpus:
         ap.error(f"--global-views {args.global_views} < --gpus {args.gpus}: every rank needs a view")
+    if args.as_rank is not None:
+        try:
+            r, n = (int(x) for x in args.as_rank.split("/"))
+        except ValueError:
+            ap.error("--as-rank takes R/N")
+        if args.global_views is None or args.gpus != 1 or not 0 <= r < n or n > args.global_views:
+            ap.error("--as-rank R/N: strong scaling on one GPU, 0 <= R < N <= --global-views")
+        args.as_rank = (r, n)
     return args
 
 
@@ -308,10 +320,11 @@ def main():
     if not strong and not 1 <= args.views_per_gpu <= native.RM_MAX_VIEWS_PER_CALL:
         raise SystemExit(f"--views-per-gpu must be in 1..{native.RM_MAX_VIEWS_PER_CALL}")
     npix = W * H
-    shard = Shard(rank, world, 0 if strong else args.views_per_gpu, 1, args.global_views or 0)
+    shard = (Shard(args.as_rank[0], args.as_rank[1], 0, 1, args.global_views) if args.as_rank is not None else
+             Shard(rank, world, 0 if strong else args.views_per_gpu, 1, args.global_views or 0))
     vpg = shard.count()  # this rank's views per step
     rays_per_rank = vpg * npix
-    rays_global = shard.views_total * npix
+    rays_global = shard.views_total * npix if args.as_rank is None else rays_per_rank
     # views per train call (one launch of up to 128 views / 33.5M rays each)
     views_per_call = max(1, min(native.RM_MAX_VIEWS_PER_CALL, MAX_RAYS_PER_CALL // npix))
     if args.views_per_call > 0:
@@ -416,7 +429,8 @@ def main():
             loss_out.copy_(tot[nm:])
 
     dp = ViewShardedStep(shard, npix, rmm.packed_size(M), "cuda", step_fn,
-                         optim_fn=None if fused_adam else (lambda g: opt.step(g, args.lr)))
+                         optim_fn=None if fused_adam else (lambda g: opt.step(g, args.lr)),
+                         collective=args.as_rank is None)
     # graph mode: progress and Adam's step from a device record the optimizer advances (the
     # eager steps of the run read it too, so eager and replayed steps compute the same thing)
     sdev = None
@@ -724,7 +738,10 @@ def main():
                        "cameras": args.cameras and os.path.relpath(os.path.abspath(args.cameras), ROOT),
                        "targets": args.targets,
                        "start_scene": args.scene_json and os.path.relpath(os.path.abspath(args.scene_json), ROOT),
-                       "parallelism": f"views-dp{world}" + ("" if backend == "nccl" else f" ({backend} rehearsal)")},
+                       "parallelism": (f"views-dp{world}" + ("" if backend == "nccl" else f" ({backend} rehearsal)")
+                                       if args.as_rank is None else
+                                       f"rank {args.as_rank[0]} of views-dp{args.as_rank[1]}, alone on one GPU "
+                                       f"(no all-reduce)")},
             "value_median": round(rays_global / (med_ms * 1e-3) / 1e6, 3),
             "value_exit_off": None if not exit_off_s else round(rays_global * args.steps / exit_off_s / 1e6, 3),
             "value_exit_off_note": "the same steps replayed untimed-by-events with the exact early exit off (every "

@@ -67,8 +67,11 @@ class ViewShardedStep:
 
     def __init__(self, shard: Shard, rays_per_view: int, num_params: int, device,
                  step_fn: Callable[[Sequence[int], float, torch.Tensor, torch.Tensor], None],
-                 optim_fn: Callable[[torch.Tensor], None] | None = None, group=None):
+                 optim_fn: Callable[[torch.Tensor], None] | None = None, group=None, collective: bool = True):
         self.shard = shard
+        # collective=False: one process runs one rank's share of a world-size-N step alone (its
+        # views and the global ray count, no all-reduce: bench.py --as-rank)
+        self.collective = collective
         self.rays_global = rays_per_view * shard.views_total
         self.inv_count = 1.0 / (3.0 * self.rays_global)
         # one buffer, one collective: [packed gradient | loss sum]
@@ -86,7 +89,7 @@ class ViewShardedStep:
     def __call__(self, step: int) -> None:
         views = self.shard.views(step)
         self.step_fn(views, self.inv_count, self.grads, self.loss)
-        if self.shard.world > 1:
+        if self.shard.world > 1 and self.collective:
             import torch.distributed as dist
             if self.time_allreduce:
                 ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))

@@ -145,3 +145,19 @@ def test_shard_counts_strong_and_weak():
         assert seen == [(4 * gv + j) % 100 for j in range(gv)]
     weak = Shard(1, 4, 10, 80)
     assert weak.count() == 10 and weak.views_total == 40
+
+
+def test_rank_share_alone_has_fixed_views_and_global_count():
+    """bench.py --as-rank R/N: one process runs rank R's share of an N-rank strong step -- the same
+    views every step when the step covers the whole ring (what rank R renders at N ranks), the
+    global ray count in the seed, and no collective (no process group exists here)."""
+    import torch
+    from burn_raymarching_amd.parallel import Shard, ViewShardedStep
+    calls, opt = [], []
+    shard = Shard(3, 8, 0, 80, 80)
+    dp = ViewShardedStep(shard, 100, 5, "cpu", lambda v, ic, g, l: calls.append((list(v), ic)),
+                         optim_fn=lambda g: opt.append(1), collective=False)
+    for step in range(3):
+        dp(step)
+    assert [c[0] for c in calls] == [list(range(30, 40))] * 3
+    assert all(c[1] == 1.0 / (3.0 * 100 * 80) for c in calls) and len(opt) == 3
