@@ -16,7 +16,9 @@ against it:
     python tools/predict_scaling.py --bench profiles/r05_bench.json --balance profiles/r04b_shard_balance.json \
         --allreduce profiles/r05b_allreduce.json [--hop-us 2.5] [--slices 2=... 4=... 8=...] \
         > profiles/r05_scaling_prediction.json
-With --slices the N-rank step is one rank's step measured on one GPU (bench.py --global-views
+With --as-rank every rank's share of the N-rank step is measured alone on one GPU (bench.py
+--as-rank R/N: its fixed views, as at N ranks) and T(N) = the slowest rank's step + the
+modelled all-reduce. With --slices the N-rank step is one rank's step measured on one GPU (bench.py --global-views
 80/N --ring 80: the rank's views in one launch with its own record, origin, reduction and
 optimizer kernels), its kernel stretched by the balance study's slowest-over-mean rank (the
 one-GPU run rotates through the ring, so it times the mean rank), plus the modelled all-reduce.
@@ -35,6 +37,11 @@ def main():
                     help="N=file pairs (e.g. 8=profiles/r06i_slice_10.json): bench lines of one rank's step at N "
                          "ranks measured on one GPU (bench.py --global-views 80/N --ring 80); where given, T(N) uses "
                          "the measured step (its train kernel and its own small kernels) instead of the scaled slice")
+    ap.add_argument("--as-rank", nargs="*", default=[],
+                    help="N=glob pairs (e.g. 8='gpurun_out/r06n/rank_*_of_8.json'): bench lines of EVERY rank's "
+                         "share of the N-rank step run alone on one GPU (bench.py --as-rank R/N: the rank's fixed "
+                         "views, its own record / origin / reduction / optimizer kernels); T(N) = the slowest "
+                         "rank's measured step + the modelled all-reduce. Takes precedence over --slices")
     ap.add_argument("--hop-us", type=float, default=2.5,
                     help="modelled latency of one xGMI ring hop of a few-KB message (no measurement on a "
                          "one-GPU box; an assumption, stated in the output)")
@@ -56,7 +63,24 @@ def main():
         n, f = pair.split("=", 1)
         measured[int(n)] = json.load(open(f))
     out["inputs"]["slices"] = {str(n): f for n, f in (p.split("=", 1) for p in args.slices)}
+    import glob
+    shares = {}
+    for pair in args.as_rank:
+        n, pat = pair.split("=", 1)
+        shares[int(n)] = [json.load(open(f)) for f in sorted(glob.glob(pat))]
+    out["inputs"]["as_rank"] = {str(n): len(v) for n, v in shares.items()}
     for n in (1, 2, 4, 8):
+        if n in shares:  # every rank's step measured alone: the slowest, plus the all-reduce
+            lines = shares[n]
+            steps = [m["ms_per_step"] for m in lines]
+            kern = [m["roofline"]["kernel_ms_per_step"] for m in lines]
+            ar_ms = (floor_us + 2 * (n - 1) * args.hop_us) * 1e-3
+            t = max(steps) + ar_ms
+            out["curve"][str(n)] = {"step_ms": round(t, 4), "rank_step_ms": [round(x, 4) for x in steps],
+                                    "rank_train_kernel_ms": [round(x, 4) for x in kern],
+                                    "train_kernel_ms": round(max(kern), 4), "allreduce_ms": round(ar_ms, 4),
+                                    "ranks_measured": len(lines), "mrays_s": round(rays / (t * 1e-3) / 1e6, 1)}
+            continue
         if n in measured:  # one rank's whole step measured on one GPU, plus the all-reduce
             m = measured[n]
             # the one-GPU run rotates through the ring, so it times the mean rank's slice; the step
