@@ -158,6 +158,8 @@ def parse():
         args.ring_order = "spread" if args.global_views is not None else "contiguous"
     if args.global_views is not None and args.global_views < args.gpus:
         ap.error(f"--global-views {args.global_views} < --gpus {args.gpus}: every rank needs a view")
+    if args.graph == "on" and args.anneal_k is not None:
+        ap.error("--graph on freezes the march parameters of the captured step: no --anneal-k")
     if args.as_rank is not None:
         try:
             r, n = (int(x) for x in args.as_rank.split("/"))
@@ -347,8 +349,6 @@ def main():
         ring = max(args.ring, shard.views_total)
         cams = [rmm.ring_cameras(ring)[a] for a in ring_order(ring, args.ring_order)]
     shard.ring = ring
-    if use_graph and args.anneal_k is not None:
-        raise SystemExit("--graph on freezes the march parameters of the captured step: no --anneal-k")
     if use_graph and shard.views_total != ring:
         # a captured step freezes its views, target slice and camera bases: replays would train the
         # captured views while eager steps rotate through the ring -- not the same run

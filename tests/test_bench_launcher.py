@@ -42,3 +42,14 @@ def test_failing_rank_fails_the_launch():
     out = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "1", "--warmup", "0"], env=env,
                          capture_output=True, text=True, timeout=300)
     assert out.returncode != 0
+
+
+def test_argument_checks_fail_before_any_gpu_work():
+    """Contradictory bench options end in argparse (exit 2) before torch or a device is touched:
+    a rank outside its world (--as-rank), --as-rank with several GPUs, a captured step with an
+    annealed k (the capture freezes the march parameters)."""
+    for extra in (["--as-rank", "8/8"], ["--as-rank", "0/4", "--gpus", "2"], ["--as-rank", "x"],
+                  ["--graph", "on", "--anneal-k", "5"]):
+        out = subprocess.run([sys.executable, BENCH] + extra, env=_env(), capture_output=True, text=True,
+                             timeout=120)
+        assert out.returncode == 2, (extra, out.stderr[-300:])
