@@ -213,8 +213,9 @@ struct KArgs {
   // cont_list_w and ends; a launch with cont_resume = that step runs the saved blocks
   // (cont_list[0..*cont_count)) from there (and may defer again at its own cont_cap). The lists
   // are kContClasses class lists of cont_stride entries each, with kContClasses counts: a deferred
-  // block goes to the class of its rays still moving (the most first), and a continuation launch
-  // runs the classes in order -- the blocks likely to march to the end start first.
+  // block goes to the class of the march steps its slowest ray is predicted to need (the most
+  // first), and a continuation launch runs the classes in order -- the blocks likely to march to
+  // the end start first.
   // cont_state: [7][cont_rays] per ray (t, lb, D_prev, t one and two steps back, gone, rho_lb) then
   // [blocks][2] per block (choice history, steps saved).
   int cont_cap, cont_resume;
