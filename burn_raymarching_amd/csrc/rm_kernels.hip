@@ -2434,8 +2434,9 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
         if (((r * U) / ncw) % nsw != 0) return true;
       return false;
     };
+    // (always inlined: as a call its array arguments went to scratch memory)
     auto finish_split = [&](int nsw, int ncw, int crank, bool in, int ncomp, const float (&p0)[8],
-                            const float (&p1)[8]) {
+                            const float (&p1)[8]) __attribute__((always_inline)) {
       __syncthreads();  // every wave is done with the sweep's images
       // the partials indexed by live rank: slot 0 in rows [0, nst), slot 1 in [nst, 2 nst) (a
       // sweep-1 partial's column 7 is 0 and not stored: 14 rows fit a wave's 15-row image)

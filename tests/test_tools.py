@@ -66,18 +66,22 @@ def test_pmc_summary_counts_the_continuation(tmp_path):
 
 
 def test_pmc_sq_summary_counts_the_continuation(tmp_path):
-    hdr = ["Kernel_Name", "Counter_Name", "Counter_Value"]
+    """Per train step: a split step's two dispatches (first launch + continuation) summed, against
+    the exit-off run's one launch per step (the mean per dispatch would halve the split step)."""
+    hdr = ["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"]
     thdr = ["Kernel_Name", "Start_Timestamp", "End_Timestamp"]
-    for d, trans in (("d1", 1000), ("n1", 4000)):
-        _write_csv(str(tmp_path / d / "run_counter_collection.csv"), hdr,
-                   [[RAY, "SQ_INSTS_VALU_TRANS_F32", trans], [CONT, "SQ_INSTS_VALU_TRANS_F32", trans],
-                    [RAY, "SQ_INSTS_VALU", 2 * trans], [CONT, "SQ_INSTS_VALU", 2 * trans]])
-        _write_csv(str(tmp_path / d / "run_kernel_trace.csv"), thdr, [[RAY, 0, 1000], [CONT, 0, 3000], [OPT, 0, 5]])
-    _write_csv(str(tmp_path / "d2" / "run_counter_collection.csv"), hdr, [[RAY, "GRBM_GUI_ACTIVE", 4000]])
+    _write_csv(str(tmp_path / "d1" / "run_counter_collection.csv"), hdr,
+               [[1, RAY, "SQ_INSTS_VALU_TRANS_F32", 1000], [2, CONT, "SQ_INSTS_VALU_TRANS_F32", 1000],
+                [1, RAY, "SQ_INSTS_VALU", 2000], [2, CONT, "SQ_INSTS_VALU", 2000]])
+    _write_csv(str(tmp_path / "d1" / "run_kernel_trace.csv"), thdr, [[RAY, 0, 1000], [CONT, 0, 3000], [OPT, 0, 5]])
+    _write_csv(str(tmp_path / "n1" / "run_counter_collection.csv"), hdr,
+               [[1, RAY, "SQ_INSTS_VALU_TRANS_F32", 8000], [1, RAY, "SQ_INSTS_VALU", 16000]])
+    _write_csv(str(tmp_path / "n1" / "run_kernel_trace.csv"), thdr, [[RAY, 0, 9000]])
+    _write_csv(str(tmp_path / "d2" / "run_counter_collection.csv"), hdr, [[1, RAY, "GRBM_GUI_ACTIVE", 4000]])
     _write_csv(str(tmp_path / "d2" / "run_kernel_trace.csv"), thdr, [[RAY, 0, 2000]])
     out = tmp_path / "sq.json"
     _tool("pmc_sq_summary.py", str(out), "K", str(tmp_path / "d1"), str(tmp_path / "d2"), str(tmp_path / "n1"))
     r = json.load(open(out))["train_kernel"]["K"]
-    assert r["kernel_ns"] == 2000.0  # the mean over both kernels' launches
-    assert r["executed_ratio_pmc"] == 0.25
+    assert r["launches"] == 1 and r["kernel_ns"] == 4000.0  # both dispatches of the one step
+    assert r["executed_ratio_pmc"] == 0.25  # (1000 + 1000) / 8000
     assert r["trans_share_of_valu"] == 0.5

@@ -6,3 +6,5 @@ export TMPDIR=/tmp
 bash tools/gpu_r06n.sh || exit 1
 mkdir -p gpurun_out/r06o
 CONFIGS="c5 c5g" ROUNDS=2 bash tools/gpu_ab.sh default "RM_SPLIT_CONT_STEPS=64" "RM_SPLIT_CONT_STEPS=80" "RM_SPLIT_CONT2_STEPS=96" "RM_STATIC_ORDER=1" 2>&1 | tee gpurun_out/r06o/ab.txt
+# (3) the backward's finish_split inlined (no scratch memory: 80 -> 0 bytes per lane) vs before (lib:scr)
+CONFIGS="m c2cj c5g" ROUNDS=2 bash tools/gpu_ab.sh lib:scr default 2>&1 | tee gpurun_out/r06o/ab_scr.txt

@@ -55,8 +55,9 @@ def counters(path):
         if not is_train(r["Kernel_Name"]):
             continue
         vals[r["Counter_Name"]] = vals.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
-        if KERNEL in r["Kernel_Name"]:
-            firsts.setdefault(r["Counter_Name"], set()).add(r["Dispatch_Id"])
+        if KERNEL in r["Kernel_Name"]:  # (one row per dispatch and counter without a dispatch id)
+            ids = firsts.setdefault(r["Counter_Name"], set())
+            ids.add(r.get("Dispatch_Id") or len(ids))
     steps = max((len(v) for v in firsts.values()), default=0)
     return {k: v / steps for k, v in vals.items()} if steps else {}, steps
 
