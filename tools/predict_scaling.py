@@ -17,8 +17,11 @@ against it:
         --allreduce profiles/r05b_allreduce.json [--hop-us 2.5] [--slices 2=... 4=... 8=...] \
         > profiles/r05_scaling_prediction.json
 With --as-rank every rank's share of the N-rank step is measured alone on one GPU (bench.py
---as-rank R/N: its fixed views, as at N ranks) and T(N) = the slowest rank's step + the
-modelled all-reduce. With --slices the N-rank step is one rank's step measured on one GPU (bench.py --global-views
+--as-rank R/N: its fixed views, as at N ranks); alone, a rank trains on its own gradient and its
+scene drifts from the all-reduced trajectory, so the prediction takes the efficiency of its launch
+(the executed roofline fraction) and applies it to 1/N of the N = 1 step's executed work:
+T(N) = kernel_1 x frac_1 / (N x frac_rank) x (slowest / mean slice) + the rank's time outside its
+train kernel + the modelled all-reduce. With --slices the N-rank step is one rank's step measured on one GPU (bench.py --global-views
 80/N --ring 80: the rank's views in one launch with its own record, origin, reduction and
 optimizer kernels), its kernel stretched by the balance study's slowest-over-mean rank (the
 one-GPU run rotates through the ring, so it times the mean rank), plus the modelled all-reduce.
@@ -70,15 +73,29 @@ def main():
         shares[int(n)] = [json.load(open(f)) for f in sorted(glob.glob(pat))]
     out["inputs"]["as_rank"] = {str(n): len(v) for n, v in shares.items()}
     for n in (1, 2, 4, 8):
-        if n in shares:  # every rank's step measured alone: the slowest, plus the all-reduce
+        if n in shares:
+            # Every rank's share measured alone. Alone, a rank's Adam sees only its own views'
+            # gradient, so its scene drifts differently from the all-reduced run's and the executed
+            # work per ray differs (measured: 0.20-0.22 vs 0.35 of the canonical FLOP); what carries
+            # over is the efficiency of the rank's launch shape (its executed roofline fraction).
+            # The rank's train kernel at the N = 1 trajectory's work: 1/N of the N = 1 step's
+            # executed FLOP at the rank's fraction, stretched by the slowest-over-mean slice of the
+            # balance study; plus the rank's measured time outside its train kernel, plus the
+            # all-reduce.
             lines = shares[n]
-            steps = [m["ms_per_step"] for m in lines]
-            kern = [m["roofline"]["kernel_ms_per_step"] for m in lines]
+            fr = [m["roofline"]["frac"] for m in lines]
+            frac_rank = sum(fr) / len(fr)
+            sl = bal[str(n)]["slice_ms"]
+            imb = max(sl) / (sum(sl) / len(sl))
+            kern = kern1 * b["roofline"]["frac"] / (n * frac_rank) * imb
+            outside_rank = max(m["ms_per_step"] - m["roofline"]["kernel_ms_per_step"] for m in lines)
             ar_ms = (floor_us + 2 * (n - 1) * args.hop_us) * 1e-3
-            t = max(steps) + ar_ms
-            out["curve"][str(n)] = {"step_ms": round(t, 4), "rank_step_ms": [round(x, 4) for x in steps],
-                                    "rank_train_kernel_ms": [round(x, 4) for x in kern],
-                                    "train_kernel_ms": round(max(kern), 4), "allreduce_ms": round(ar_ms, 4),
+            t = kern + outside_rank + ar_ms
+            out["curve"][str(n)] = {"step_ms": round(t, 4), "train_kernel_ms": round(kern, 4),
+                                    "rank_frac_measured": [round(x, 4) for x in fr],
+                                    "rank_executed_frac_measured": [m["roofline"]["executed_frac"] for m in lines],
+                                    "rank_outside_ms_measured": round(outside_rank, 4),
+                                    "slowest_over_mean_rank": round(imb, 4), "allreduce_ms": round(ar_ms, 4),
                                     "ranks_measured": len(lines), "mrays_s": round(rays / (t * 1e-3) / 1e6, 1)}
             continue
         if n in measured:  # one rank's whole step measured on one GPU, plus the all-reduce
