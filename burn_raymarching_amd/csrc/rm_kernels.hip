@@ -3581,23 +3581,13 @@ struct rm_context {
   long long stats_waves = 0;                // their ray waves (a split block holds one)
   int* block_order = nullptr;               // centre-out tile order for order_tx x order_ty tiles
   int order_tx = 0, order_ty = 0, order_sub = 0;
-  // Cost-ordered dispatch, one slot per view set (geometry + camera poses) up to kOrderSlots,
-  // least recently used replaced: a caller that rotates through a ring of views finds each view
-  // set's own order from its last visit. A slot: 3 x [class][kMaxBlocksPerLaunch] block lists,
-  // 3 x [class] list lengths (zeroed one launch ahead) and the device turn word after them.
-  struct OrderSlot {
-    int* olist = nullptr;
-    int* ocnt = nullptr;
-    int* oturn = nullptr;               // device word: the list set the next keyed launch appends to
-    unsigned long long key = 0;         // the view set of the slot's last keyed launch
-    bool valid = false;                 // its lists order the next launch of that key
-    unsigned long long used = 0;        // LRU clock
-  };
-  std::vector<OrderSlot> oslots;
-  unsigned long long oclock = 0;
-  int* ocnt = nullptr;                      // the last keyed launch's slot's counts (rm_debug_order_counts)
+  int* olist = nullptr;                     // cost-ordered dispatch: 3 x [class][kMaxBlocksPerLaunch] block lists
+  int* ocnt = nullptr;                      // 3 x [class] list lengths (zeroed one launch ahead)
   float* cont_buf = nullptr;                // split continuation: saved march state | list | count
   size_t cont_bytes = 0;
+  int* oturn = nullptr;                     // device word: the list set the next keyed launch appends to
+  unsigned long long cost_key = 0;          // geometry of the last keyed launch (its lists order the next)
+  bool cost_valid = false;
 #ifdef RM_BLOCK_TRACE
   unsigned long long* btrace = nullptr;     // measurement build: per-wave records of the last launch
   long long btrace_waves = 0;
@@ -3810,47 +3800,6 @@ struct Call {
   };
   const Adam* adam = nullptr;
 };
-
-// The cost order's view set: a keyed launch's geometry key mixed with the call's camera poses
-// (FNV-1a over the rm_camera records), so that each view set keeps its own order.
-unsigned long long order_key_views(unsigned long long key, const Call& c) {
-  if (!c.cam || !c.cams || c.views <= 0) return key;
-  unsigned long long h = 1469598103934665603ull ^ key;
-  const unsigned char* p = reinterpret_cast<const unsigned char*>(c.cams);
-  for (size_t i = 0; i < sizeof(rm_camera) * (size_t)c.views; ++i) h = (h ^ p[i]) * 1099511628211ull;
-  return h | 1ull;  // never 0 (0 = no key)
-}
-
-// The order slot of a view set: its own if present, else a new one (up to kOrderSlots), else the
-// least recently used one, taken over (its lists then order nothing: slot->valid stays false for
-// the new key, and the sets' rotation carries on from the slot's turn word).
-constexpr int kOrderSlots = 12;
-int order_slot(rm_context* ctx, unsigned long long key, rm_context::OrderSlot*& out) {
-  constexpr int kCls = RM_ORDER_CLASSES;
-  rm_context::OrderSlot* hit = nullptr;
-  for (auto& sl : ctx->oslots)
-    if (sl.valid && sl.key == key) hit = &sl;
-  if (!hit && (int)ctx->oslots.size() < kOrderSlots) {
-    rm_context::OrderSlot sl;
-    RM_HIP(ctx, hipMalloc(&sl.olist, sizeof(int) * 3 * kCls * kMaxBlocksPerLaunch));
-    // the three sets' counts, then the turn word, RM_ORDER_CNT_STRIDE ints apart
-    RM_HIP(ctx, hipMalloc(&sl.ocnt, sizeof(int) * 4 * RM_ORDER_CNT_STRIDE));
-    RM_HIP(ctx, hipMemsetAsync(sl.ocnt, 0, sizeof(int) * 4 * RM_ORDER_CNT_STRIDE, ctx->stream));
-    sl.oturn = sl.ocnt + 3 * RM_ORDER_CNT_STRIDE;
-    ctx->oslots.push_back(sl);
-    hit = &ctx->oslots.back();
-  }
-  if (!hit) {
-    hit = &ctx->oslots[0];
-    for (auto& sl : ctx->oslots)
-      if (sl.used < hit->used) hit = &sl;
-    hit->valid = false;
-  }
-  hit->used = ++ctx->oclock;
-  out = hit;
-  return RM_OK;
-}
-
 
 FinalArgs final_args(const Call& c, bool first) {
   const rm_grads* gp = c.grads;
@@ -4305,29 +4254,35 @@ int run(rm_context* ctx, const Call& c) {
     // cost-ordered dispatch from the previous launch over the same views (single-launch calls)
     const bool has_rec = c.mode == kBwd || c.mode == kTrain;
     unsigned long long key = 0;
-    rm_context::OrderSlot* slot = nullptr;
     if (a.block_order != nullptr && has_rec && nb == blocks_left && done == 0 &&
         (c.march->flags & RM_MARCH_STATIC_ORDER) == 0) {
       key = ((unsigned long long)c.W << 48) ^ ((unsigned long long)c.H << 32) ^ ((unsigned long long)c.views << 24) ^
             ((unsigned long long)Mpad << 1) ^ 1ull ^ ((unsigned long long)split << 2);
-      key = order_key_views(key, c);
-      if ((rc = order_slot(ctx, key, slot)) != RM_OK) return rc;
+      constexpr int kCls = RM_ORDER_CLASSES;
+      if (!ctx->olist) {
+        RM_HIP(ctx, hipMalloc(&ctx->olist, sizeof(int) * 3 * kCls * kMaxBlocksPerLaunch));
+        // the three sets' counts, then the turn word, RM_ORDER_CNT_STRIDE ints apart
+        RM_HIP(ctx, hipMalloc(&ctx->ocnt, sizeof(int) * 4 * RM_ORDER_CNT_STRIDE));
+        RM_HIP(ctx, hipMemsetAsync(ctx->ocnt, 0, sizeof(int) * 4 * RM_ORDER_CNT_STRIDE, ctx->stream));
+        ctx->oturn = ctx->ocnt + 3 * RM_ORDER_CNT_STRIDE;
+      }
       // three list sets in rotation: the previous launch's (read), this launch's (appended;
       // cleared by the previous launch) and the next launch's (cleared by this one); which is which
       // the kernel reads from the device turn word, advanced by this call's reduction (order_sets)
-      if (slot->valid && slot->key == key) {
-        a.olist_r = slot->olist;
-        a.ocnt_r = slot->ocnt;
+      if (ctx->cost_valid && ctx->cost_key == key) {
+        a.olist_r = ctx->olist;
+        a.ocnt_r = ctx->ocnt;
       }
-      a.olist_w = slot->olist;
-      a.ocnt_w = slot->ocnt;
-      a.ocnt_z = slot->ocnt;
-      a.oturn = slot->oturn;
-      ctx->ocnt = slot->ocnt;
+      a.olist_w = ctx->olist;
+      a.ocnt_w = ctx->ocnt;
+      a.ocnt_z = ctx->ocnt;
+      a.oturn = ctx->oturn;
       if (const char* e = std::getenv("RM_DEBUG_SKIP_ORDER_CLEAR"))  // recovery test (rm_debug_order_counts)
         if (e[0] == '1') a.ocnt_z = nullptr;
-      slot->valid = true;
-      slot->key = key;
+    }
+    if (has_rec) {
+      ctx->cost_valid = key != 0;
+      ctx->cost_key = key;
     }
     if (nb > 0 && a.cull) {
       if (!ctx->esc_flags) RM_HIP(ctx, hipMalloc(&ctx->esc_flags, sizeof(int) * kMaxBlocksPerLaunch));
@@ -4548,16 +4503,14 @@ int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset) {
 
 void rm_destroy(rm_context* ctx) {
   if (!ctx) return;
-  if (ctx->stats_dev || ctx->esc_flags || ctx->rec || ctx->block_order || !ctx->oslots.empty() || ctx->cont_buf) {
+  if (ctx->stats_dev || ctx->esc_flags || ctx->rec || ctx->block_order || ctx->olist || ctx->cont_buf) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stats_dev) (void)hipFree(ctx->stats_dev);
     if (ctx->esc_flags) (void)hipFree(ctx->esc_flags);
     if (ctx->block_order) (void)hipFree(ctx->block_order);
-    for (auto& sl : ctx->oslots) {
-      (void)hipFree(sl.olist);
-      (void)hipFree(sl.ocnt);
-    }
+    if (ctx->olist) (void)hipFree(ctx->olist);
     if (ctx->cont_buf) (void)hipFree(ctx->cont_buf);
+    if (ctx->ocnt) (void)hipFree(ctx->ocnt);
     if (ctx->rec) (void)hipFree(ctx->rec);
   }
   if (ctx->arrivals || ctx->red_arrivals || ctx->batch || ctx->cams_dev || ctx->opt_pre || ctx->opt_arrival) {
