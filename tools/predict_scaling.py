@@ -16,6 +16,10 @@ against it:
     python tools/predict_scaling.py --bench profiles/r05_bench.json --balance profiles/r04b_shard_balance.json \
         --allreduce profiles/r05b_allreduce.json [--hop-us 2.5] [--slices 2=... 4=... 8=...] \
         > profiles/r05_scaling_prediction.json
+With --per-call the N = 1 step is run as N calls of 80/N views (bench.py --views-per-call 80/N):
+each call's launch is what one rank's launch is at N ranks, on the same (all-reduced) trajectory;
+T(N) = one call's train kernel x (slowest / mean slice) + one call's share of the step's other
+kernels + the modelled all-reduce.
 With --as-rank every rank's share of the N-rank step is measured alone on one GPU (bench.py
 --as-rank R/N: its fixed views, as at N ranks); alone, a rank trains on its own gradient and its
 scene drifts from the all-reduced trajectory, so the prediction takes the efficiency of its launch
@@ -45,6 +49,12 @@ def main():
                          "share of the N-rank step run alone on one GPU (bench.py --as-rank R/N: the rank's fixed "
                          "views, its own record / origin / reduction / optimizer kernels); T(N) = the slowest "
                          "rank's measured step + the modelled all-reduce. Takes precedence over --slices")
+    ap.add_argument("--per-call", nargs="*", default=[],
+                    help="N=file pairs: bench lines of the N = 1 step run as N calls of 80/N views "
+                         "(bench.py --views-per-call 80/N: each call its own launch, context and cost "
+                         "order, all on the N = 1 trajectory); T(N) = one call's train kernel x the "
+                         "slowest-over-mean slice + one call's share of the other kernels + the "
+                         "all-reduce. Takes precedence over --as-rank and --slices")
     ap.add_argument("--hop-us", type=float, default=2.5,
                     help="modelled latency of one xGMI ring hop of a few-KB message (no measurement on a "
                          "one-GPU box; an assumption, stated in the output)")
@@ -66,6 +76,11 @@ def main():
         n, f = pair.split("=", 1)
         measured[int(n)] = json.load(open(f))
     out["inputs"]["slices"] = {str(n): f for n, f in (p.split("=", 1) for p in args.slices)}
+    percall = {}
+    for pair in args.per_call:
+        n, f = pair.split("=", 1)
+        percall[int(n)] = json.load(open(f))
+    out["inputs"]["per_call"] = {str(n): f for n, f in (p.split("=", 1) for p in args.per_call)}
     import glob
     shares = {}
     for pair in args.as_rank:
@@ -73,6 +88,23 @@ def main():
         shares[int(n)] = [json.load(open(f)) for f in sorted(glob.glob(pat))]
     out["inputs"]["as_rank"] = {str(n): len(v) for n, v in shares.items()}
     for n in (1, 2, 4, 8):
+        if n in percall and n > 1:
+            # one rank's launch on the N = 1 trajectory: the step's N calls each a rank's views
+            m = percall[n]
+            r = m["roofline"]
+            calls = n  # calls per step
+            sl = bal[str(n)]["slice_ms"]
+            imb = max(sl) / (sum(sl) / len(sl))
+            kern = r["kernel_ms"] * imb  # per launch (= per call)
+            other = (m["ms_per_step"] - r["kernel_ms_per_step"]) / calls
+            ar_ms = (floor_us + 2 * (n - 1) * args.hop_us) * 1e-3
+            t = kern + other + ar_ms
+            out["curve"][str(n)] = {"step_ms": round(t, 4), "train_kernel_ms": round(kern, 4),
+                                    "call_kernel_ms_measured": r["kernel_ms"], "call_frac_measured": r["frac"],
+                                    "call_other_ms_measured": round(other, 4),
+                                    "slowest_over_mean_rank": round(imb, 4), "allreduce_ms": round(ar_ms, 4),
+                                    "mrays_s": round(rays / (t * 1e-3) / 1e6, 1)}
+            continue
         if n in shares:
             # Every rank's share measured alone. Alone, a rank's Adam sees only its own views'
             # gradient, so its scene drifts differently from the all-reduced run's and the executed
