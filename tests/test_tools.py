@@ -85,3 +85,24 @@ def test_pmc_sq_summary_counts_the_continuation(tmp_path):
     assert r["launches"] == 1 and r["kernel_ns"] == 4000.0  # both dispatches of the one step
     assert r["executed_ratio_pmc"] == 0.25  # (1000 + 1000) / 8000
     assert r["trans_share_of_valu"] == 0.5
+
+
+def test_predict_scaling_per_call(tmp_path):
+    """tools/predict_scaling.py --per-call: T(N) = one call's train kernel (the N = 1 step run as N
+    calls) x the slowest-over-mean slice + one call's share of the step's other kernels + the
+    all-reduce floor + 2 (N - 1) hops; efficiency against the N = 1 line."""
+    def line(ms, kern_step, kern, launches):
+        return {"ms_per_step": ms, "config": {"spheres": 256, "rays_per_step": 8_000_000},
+                "roofline": {"kernel_ms_per_step": kern_step, "kernel_ms": kern, "launches_timed": launches,
+                             "frac": 0.5}}
+    json.dump(line(10.0, 9.8, 9.8, 6), open(tmp_path / "n1.json", "w"))
+    json.dump(line(10.4, 10.0, 5.0, 12), open(tmp_path / "n2.json", "w"))
+    json.dump({"spread": {"2": {"slice_ms": [1.0, 1.02]}}}, open(tmp_path / "bal.json", "w"))
+    json.dump({"allreduce": {"256": {"median_us": 15.0}}}, open(tmp_path / "ar.json", "w"))
+    out = _tool("predict_scaling.py", "--bench", str(tmp_path / "n1.json"), "--balance", str(tmp_path / "bal.json"),
+                "--allreduce", str(tmp_path / "ar.json"), "--per-call", f"2={tmp_path / 'n2.json'}")
+    c = json.loads(out)["curve"]["2"]
+    imb = 1.02 / 1.01
+    t = 5.0 * imb + 0.4 / 2 + (15.0 + 2 * 2.5) * 1e-3
+    assert abs(c["step_ms"] - round(t, 4)) < 1e-9
+    assert abs(c["efficiency"] - round(8.0 / t * 1e3 / (2 * 800.0), 3)) <= 1e-3

@@ -144,6 +144,8 @@ def main():
                                     "slowest_over_mean_rank": round(imb, 4), "allreduce_ms": round(ar_ms, 4),
                                     "mrays_s": round(rays / (t * 1e-3) / 1e6, 1)}
             continue
+        if n > 1 and str(n) not in bal:  # no measurement for this N
+            continue
         slice_ms = kern1 if n == 1 else max(bal[str(n)]["slice_ms"])
         # the balance study timed each rank's slice as its own launch (as the rank runs it), on a
         # scene earlier in training than the bench's timed steps: its slices are scaled by the
@@ -155,7 +157,7 @@ def main():
         out["curve"][str(n)] = {"step_ms": round(t, 4), "train_kernel_ms": round(slice_ms, 4),
                                 "allreduce_ms": round(ar_ms, 4), "mrays_s": round(rays / (t * 1e-3) / 1e6, 1)}
     v1 = out["curve"]["1"]["mrays_s"]
-    for n in ("2", "4", "8"):
+    for n in (k for k in ("2", "4", "8") if k in out["curve"]):
         out["curve"][n]["efficiency"] = round(out["curve"][n]["mrays_s"] / (int(n) * v1), 3)
     print(json.dumps(out, indent=1))
 
