@@ -3688,6 +3688,13 @@ int split_cont_steps(int steps) {
   if (const char* e = std::getenv("RM_SPLIT_CONT_STEPS")) return std::max(0, std::atoi(e));
   return steps >= 64 ? std::max(32, 3 * steps / 8) : 0;
 }
+// The second continuation (a third launch) from S >= 128: at 3S/4 the blocks still marching are
+// dealt out again over the CUs (C5 / C5g with 32-ray groups, three rounds on one box: +2.5 % /
+// +3.5 % at 96 of 128 steps, profiles/r06_ab.txt r06r). 0 = none; env RM_SPLIT_CONT2_STEPS.
+int split_cont2_steps(int steps) {
+  if (const char* e = std::getenv("RM_SPLIT_CONT2_STEPS")) return std::max(0, std::atoi(e));
+  return steps >= 128 ? 3 * steps / 4 : 0;
+}
 
 size_t ws_need(long long max_rays, int M, int rays_per_block = kBlock) {
   const int Mpad = pad_spheres(M);
@@ -4310,8 +4317,7 @@ int run(rm_context* ctx, const Call& c) {
       // first launch placed them by a cost order that only partly predicts which 64-ray groups
       // march every step. Bit-identical to one launch (tests/test_gpu_split.py).
       // up to two continuations: at split_cont_steps(S) and (env RM_SPLIT_CONT2_STEPS) later
-      int caps[2] = {split_cont_steps(a.steps), 0};
-      if (const char* e = std::getenv("RM_SPLIT_CONT2_STEPS")) caps[1] = std::max(0, std::atoi(e));
+      int caps[2] = {split_cont_steps(a.steps), split_cont2_steps(a.steps)};
       const bool cont = split && c.mode != kRender && c.mode != kFwd && a.early_exit && caps[0] > 0 &&
                         a.steps >= 2 * caps[0];
       if (!(caps[1] > caps[0] && caps[1] < a.steps)) caps[1] = 0;

@@ -180,7 +180,8 @@ def test_split_threshold(rm, monkeypatch, m, views, size, split):
 
 def test_split_continuation(rm, oracle, monkeypatch):
     """Continuation launch (split train / backward launches with S >= 64: the blocks still marching
-    at step max(32, 3S/8) stop, and a second launch runs them from their saved march state):
+    at step max(32, 3S/8) stop, and a second launch runs them from their saved march state; from
+    S >= 128 a third from 3S/4):
     bit-identical to one launch (RM_SPLIT_CONT_STEPS=0), to other continuation steps and to the
     march with the early exit off; the timed launches show the second launch; the image is within
     the oracle's tolerance."""
@@ -214,6 +215,17 @@ def test_split_continuation(rm, oracle, monkeypatch):
     assert ctx.collect_timing(reset=True)[1] == 3
     monkeypatch.delenv("RM_SPLIT_CONT2_STEPS")
     _equal(base, _train(render, native, cams, W, H, tg, s, K, S, flags=native.RM_MARCH_NO_EARLY_EXIT))
+    # from S = 128 the default takes the second continuation too (at 3S/4): three launches, the
+    # one launch's bits
+    tg2 = render.render_diff_camera(cams, W, H, model.scene_tensors(model.synthetic_scene(M, 24)), K, 128)
+    ctx.collect_timing(reset=True)
+    ctx.timing(True)
+    b128 = _train(render, native, cams, W, H, tg2, s, K, 128)
+    ctx.timing(False)
+    assert ctx.collect_timing(reset=True)[1] == 3
+    monkeypatch.setenv("RM_SPLIT_CONT_STEPS", "0")
+    _equal(b128, _train(render, native, cams, W, H, tg2, s, K, 128))
+    monkeypatch.delenv("RM_SPLIT_CONT_STEPS")
     o, d = cam_rays(oracle, cams, W, H)
     check_fwd(base[2].reshape(-1, 3), oracle.render_diff(o.astype(np.float64), d.astype(np.float64), sc, S, K))
     # the backward mode continues the same way (ragged: 3 views of 40x24 = 90 blocks of 32 rays)
