@@ -3695,6 +3695,28 @@ int split_cont2_steps(int steps) {
   if (const char* e = std::getenv("RM_SPLIT_CONT2_STEPS")) return std::max(0, std::atoi(e));
   return steps >= 128 ? 3 * steps / 4 : 0;
 }
+// The continuation steps of a split launch, increasing, each < steps: caps[0..n), caps[n] = 0.
+// Env RM_SPLIT_CONT_LIST="48,80,112" replaces the rule (up to kMaxCont steps).
+constexpr int kMaxCont = 4;
+int split_cont_caps(int steps, int (&caps)[kMaxCont + 1]) {
+  int n = 0;
+  if (const char* e = std::getenv("RM_SPLIT_CONT_LIST")) {
+    for (const char* q = e; *q && n < kMaxCont;) {
+      const int v = std::atoi(q);
+      if (v > 0 && v < steps && (n == 0 || v > caps[n - 1])) caps[n++] = v;
+      while (*q && *q != ',') ++q;
+      if (*q == ',') ++q;
+    }
+  } else {
+    const int c0 = split_cont_steps(steps), c1 = split_cont2_steps(steps);
+    if (c0 > 0 && c0 < steps) {
+      caps[n++] = c0;
+      if (c1 > c0 && c1 < steps) caps[n++] = c1;
+    }
+  }
+  for (int i = n; i <= kMaxCont; ++i) caps[i] = 0;
+  return n;
+}
 
 size_t ws_need(long long max_rays, int M, int rays_per_block = kBlock) {
   const int Mpad = pad_spheres(M);
@@ -4316,11 +4338,13 @@ int run(rm_context* ctx, const Call& c) {
       // state, dispatched one after another at its front -- spread evenly over the CUs, where the
       // first launch placed them by a cost order that only partly predicts which 64-ray groups
       // march every step. Bit-identical to one launch (tests/test_gpu_split.py).
-      // up to two continuations: at split_cont_steps(S) and (env RM_SPLIT_CONT2_STEPS) later
-      int caps[2] = {split_cont_steps(a.steps), split_cont2_steps(a.steps)};
-      const bool cont = split && c.mode != kRender && c.mode != kFwd && a.early_exit && caps[0] > 0 &&
+      // continuations at increasing steps (split_cont_caps): launch k resumes the blocks the
+      // previous launch deferred (list k % 2) and defers, at the next step of the list, into list
+      // (k + 1) % 2, whose counts are cleared before it runs
+      int caps[kMaxCont + 1];
+      const int ncaps = split_cont_caps(a.steps, caps);
+      const bool cont = split && c.mode != kRender && c.mode != kFwd && a.early_exit && ncaps > 0 &&
                         a.steps >= 2 * caps[0];
-      if (!(caps[1] > caps[0] && caps[1] < a.steps)) caps[1] = 0;
       int* lists[2] = {nullptr, nullptr};
       int* counts[2] = {nullptr, nullptr};
       if (cont) {
@@ -4353,14 +4377,16 @@ int run(rm_context* ctx, const Call& c) {
       else if (c.mode == kTrain) launch_ray<kTrain>(c.cam, split, grid, lds, ctx->stream, a, ev0, ev1);
       else launch_ray<kRender>(c.cam, false, grid, lds, ctx->stream, a, ev0, ev1);
       RM_HIP(ctx, hipGetLastError());
-      for (int ph = 0; cont && ph < 2 && caps[ph] > 0; ++ph) {
+      for (int ph = 0; cont && ph < ncaps; ++ph) {
         KArgs b = a;
         b.cont_resume = caps[ph];
-        b.cont_list = lists[ph];
-        b.cont_count = counts[ph];
-        b.cont_cap = ph == 0 ? caps[1] : 0;  // the second continuation, if any
-        b.cont_list_w = lists[1];
-        b.cont_count_w = counts[1];
+        b.cont_list = lists[ph & 1];
+        b.cont_count = counts[ph & 1];
+        b.cont_cap = caps[ph + 1];  // the next continuation, if any (0: none)
+        b.cont_list_w = lists[(ph + 1) & 1];
+        b.cont_count_w = counts[(ph + 1) & 1];
+        if (ph > 0 && b.cont_cap > 0)  // list (ph + 1) % 2 was read by launch ph - 1: clear its counts
+          RM_HIP(ctx, hipMemsetAsync(b.cont_count_w, 0, kContClasses * sizeof(int), ctx->stream));
         b.ocnt_z = nullptr;  // cleared by the first launch
         b.olist_r = nullptr;
         b.ocnt_r = nullptr;

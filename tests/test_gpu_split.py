@@ -226,6 +226,14 @@ def test_split_continuation(rm, oracle, monkeypatch):
     monkeypatch.setenv("RM_SPLIT_CONT_STEPS", "0")
     _equal(b128, _train(render, native, cams, W, H, tg2, s, K, 128))
     monkeypatch.delenv("RM_SPLIT_CONT_STEPS")
+    # four continuations (RM_SPLIT_CONT_LIST: the deferred lists alternate, each cleared ahead)
+    monkeypatch.setenv("RM_SPLIT_CONT_LIST", "40,72,96,112")
+    ctx.collect_timing(reset=True)
+    ctx.timing(True)
+    _equal(b128, _train(render, native, cams, W, H, tg2, s, K, 128))
+    ctx.timing(False)
+    assert ctx.collect_timing(reset=True)[1] == 5
+    monkeypatch.delenv("RM_SPLIT_CONT_LIST")
     o, d = cam_rays(oracle, cams, W, H)
     check_fwd(base[2].reshape(-1, 3), oracle.render_diff(o.astype(np.float64), d.astype(np.float64), sc, S, K))
     # the backward mode continues the same way (ragged: 3 views of 40x24 = 90 blocks of 32 rays)
