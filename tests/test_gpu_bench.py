@@ -63,3 +63,18 @@ def test_graph_refuses_rotating_views():
                           "--ring", "10", "--width", "64", "--height", "64", "--steps", "2", "--cpu-baseline", "off"],
                          cwd=ROOT, capture_output=True, text=True, timeout=110)
     assert out.returncode != 0 and "--graph on needs the same views every step" in out.stderr, out.stderr[-2000:]
+
+
+def test_bench_annealed_k_and_rank_share():
+    """--anneal-k K0 (train.rs:174's schedule over the timed steps) is named in the workload and the
+    config; --as-rank R/N runs rank R's fixed share of an N-rank strong step alone (its views, its
+    rays in value); the backward sweeps' ray shares are reported and bounded."""
+    d = _bench("--steps", "3", "--warmup", "1", "--width", "64", "--height", "64", "--global-views", "4",
+               "--ring", "4", "--anneal-k", "5", "--cpu-baseline", "off")
+    assert d["config"]["anneal_k_from"] == 5.0 and "k annealed 5->32" in d["config"]["workload"]
+    bw = d["roofline"]["backward_rays_frac"]
+    assert bw is not None and 0 < bw[1] <= bw[0] <= 1
+    d = _bench("--steps", "3", "--warmup", "1", "--width", "64", "--height", "64", "--global-views", "8",
+               "--ring", "8", "--as-rank", "1/4", "--cpu-baseline", "off")
+    assert d["config"]["rays_per_step"] == 2 * 64 * 64 and "rank 1 of views-dp4" in d["config"]["parallelism"]
+    assert abs(d["value"] - 2 * 64 * 64 / (d["ms_per_step"] * 1e-3) / 1e6) <= 0.01 * d["value"]
