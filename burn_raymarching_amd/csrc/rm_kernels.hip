@@ -52,6 +52,11 @@
 #ifndef RM_BWD_PSQ_REG
 #define RM_BWD_PSQ_REG 0  // backward sweeps form |p|^2 from p in registers (1) or read it from LDS (0)
 #endif
+#ifndef RM_DEAD_EARLY
+// backward modes: a wave whose rays all escaped ends at the hand-off instead of waiting at its
+// barrier (A/B switch; measured equal, Appendix A of DESIGN.md)
+#define RM_DEAD_EARLY 0
+#endif
 #ifndef RM_MARCH_SCHED
 #define RM_MARCH_SCHED 1  // scheduling barriers in the matrix-core march loop (0: compiler's order)
 #endif
@@ -272,6 +277,7 @@ __host__ __device__ inline size_t tiles_offset(int npairs, int nprep) {
 // Then the escape thresholds of the march: kEscTab floats (see write_bound).
 constexpr int kEscTab = 64;
 constexpr int kStatsWords = 6;  // rm_stats device counters (KArgs::stats)
+constexpr int kDeadCountSlot = 44;  // Lds::misc int: the hand-off's count of waves that ended early
 __host__ __device__ inline size_t esc_offset(int npairs, int nprep) {
   const size_t nrb = (size_t)npairs / 8;
   return tiles_offset(npairs, nprep) + nrb * 64 * 16 + nrb * 32 * sizeof(float);
@@ -1673,6 +1679,13 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     escaped_block<MODE>(a, L, blk, ri, valid, tid, lane, wave);
     return;
   }
+#if RM_DEAD_EARLY
+  if constexpr (!SPLIT && (MODE == kBwd || MODE == kTrain)) {
+    // the hand-off's count of the waves that end early: zero before any wave can reach it
+    if (tid == 0) reinterpret_cast<int*>(L.misc)[kDeadCountSlot] = 0;
+    __syncthreads();
+  }
+#endif
 
   // Scene radius bounds from the record header: with r_min, a lower bound on the scene distance
   // proves rho_j = dist_j + r_j >= kSafeRho for every sphere, so max(q, 1e-6) cannot bind and
@@ -2313,38 +2326,65 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       wflag[kWaves + wave] = steps_saved;
     }
   }
-  __syncthreads();
-  if (a.ocnt_w != nullptr && tid == 0) {
-    // the block's cost in march-step units: steps its waves ran, + kPostCost per wave that runs
-    // the post-march forward and the backward (the next call's cost-ordered dispatch)
-    int cost = 0;
+  // the block's hand-off work, by one wave once every wave has published: the cost in march-step
+  // units (steps its waves ran, + kPostCost per wave that runs the post-march forward and the
+  // backward: the next call's cost-ordered dispatch) and the work statistics
+  auto handoff_work = [&]() {
+    if (a.ocnt_w != nullptr) {
+      int cost = 0;
 #pragma unroll
-    for (int w = 0; w < (SPLIT ? 1 : kWaves); ++w) cost += a.steps - wflag[kWaves + w] + (wflag[w] ? 0 : kPostCost);
-    order_append(a, blk, cost);
-  }
-  if (a.stats != nullptr && tid == 0) {
-    int ex = 0, sv = 0;
-#pragma unroll
-    for (int w = 0; w < (SPLIT ? 1 : kWaves); ++w) {
-      ex += wflag[w];
-      sv += wflag[kWaves + w];
+      for (int w = 0; w < (SPLIT ? 1 : kWaves); ++w) cost += a.steps - wflag[kWaves + w] + (wflag[w] ? 0 : kPostCost);
+      order_append(a, blk, cost);
     }
-    if (ex != 0) atomicAdd(a.stats + 1, (unsigned long long)ex);
-    if (sv != 0) atomicAdd(a.stats + 2, (unsigned long long)sv);
+    if (a.stats != nullptr) {
+      int ex = 0, sv = 0;
+#pragma unroll
+      for (int w = 0; w < (SPLIT ? 1 : kWaves); ++w) {
+        ex += wflag[w];
+        sv += wflag[kWaves + w];
+      }
+      if (ex != 0) atomicAdd(a.stats + 1, (unsigned long long)ex);
+      if (sv != 0) atomicAdd(a.stats + 2, (unsigned long long)sv);
+    }
+  };
+  // the whole block escaped: scalar totals, live flag 0 (the reduction skips the per-sphere
+  // columns, all zero)
+  auto escaped_record = [&]() {
+    if (lane < 8) {
+      float acc = wscal[lane];
+#pragma unroll
+      for (int w = 1; w < (SPLIT ? kSplitWaves : kWaves); ++w) acc += wscal[w * 8 + lane];
+      rec[(long long)a.Mpad * 8 + lane] = acc;
+    }
+  };
+#if RM_DEAD_EARLY
+  if constexpr (!SPLIT) {
+    if (dead) {
+      // This wave's rays all escaped and its sums are published: it ends here rather than at the
+      // barrier below (an ended wave no longer counts in s_barrier), so its slot is free while the
+      // block's other waves march on. The count of such waves says which one was last; when every
+      // wave of the block left early, that one does the block's hand-off work (the others'
+      // publications precede their adds to the count: LDS operations of a wave run in order).
+      int* dcnt = reinterpret_cast<int*>(L.misc) + kDeadCountSlot;
+      int prev = 0;
+      if (lane == 0) prev = __hip_atomic_fetch_add(dcnt, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP);
+      prev = __shfl(prev, 0);
+      if (prev != kWaves - 1) return;
+      if (lane == 0) handoff_work();
+      escaped_record();
+      return;
+    }
   }
+#endif
+  __syncthreads();
   int alive = 0;
 #pragma unroll
   for (int w = 0; w < (SPLIT ? kSplitWaves : kWaves); ++w) alive |= wflag[w] ? 0 : (1 << w);
   alive = __builtin_amdgcn_readfirstlane(alive);  // block-uniform: scalar for the compiler
+  // the hand-off work: the block's first live wave (wave 0 when every wave escaped)
+  if (lane == 0 && wave == (alive != 0 ? __builtin_ctz(alive) : 0)) handoff_work();
   if (dead) {
-    if (alive == 0 && wave == 0) {  // the whole block escaped: scalar totals, live flag 0 (the
-      if (lane < 8) {               // reduction skips the per-sphere columns, all zero)
-        float acc = wscal[lane];
-#pragma unroll
-        for (int w = 1; w < (SPLIT ? kSplitWaves : kWaves); ++w) acc += wscal[w * 8 + lane];
-        rec[(long long)a.Mpad * 8 + lane] = acc;
-      }
-    }
+    if (alive == 0 && wave == 0) escaped_record();
     return;
   }
   const int arank = __popc(alive & ((1 << wave) - 1));
