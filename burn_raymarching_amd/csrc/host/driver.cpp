@@ -255,7 +255,7 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
 
   Gpu g;
   if ((rc = g.open(cfg->device)) != RMH_OK) return rc;
-  DevBuf d_org, d_dir, d_tgt, d_fg, b_org, b_dir, b_tgt;
+  DevBuf d_org, d_dir, d_tgt, d_fg;
   HIPCHK(d_org.alloc(sizeof(float) * 3 * P));
   HIPCHK(d_dir.alloc(sizeof(float) * 3 * P));
   HIPCHK(d_tgt.alloc(sizeof(float) * 3 * P));
@@ -265,10 +265,8 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
   // this rank's share of the batch (B/P rays per rank, the remainder spread)
   auto share = [&](int32_t q) { return cfg->batch / world + (q < cfg->batch % world ? 1 : 0); };
   const int32_t B = share(rank);
-  HIPCHK(b_org.alloc(sizeof(float) * 3 * (size_t)B));
-  HIPCHK(b_dir.alloc(sizeof(float) * 3 * (size_t)B));
-  HIPCHK(b_tgt.alloc(sizeof(float) * 3 * (size_t)B));
-  // the foreground list of the dataset, for the device sampler (rm_sample_batch)
+  // the foreground list of the dataset, for the device sampler (rm_train_step_sampled /
+  // rm_train_iteration draw the batch from it)
   const int32_t* h_fg = nullptr;
   int64_t n_fg_list = 0;
   rmh_dataset_fg(ds.get(), &h_fg, &n_fg_list);
@@ -341,7 +339,6 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
       // sample_batch (dataset.rs:47-82) on the device: the count rule, then draw + gather
       int64_t n_uni = 0, n_boost = 0;
       rmh_dataset_sample_count(ds.get(), B, uniform_ratio, &n_uni, &n_boost);
-      const int64_t n = n_uni + n_boost;
       // the global ray count of this step: every rank's share under the same count rule
       int64_t n_global = 0;
       for (int32_t q = 0; q < world; ++q) {
@@ -362,11 +359,10 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
                                         d_act.f(), d_grad.f(), d_raw.f(), d_m.f(), d_v.f(), M, step, (float)lr,
                                         cfg->weight_decay, 1, d_loss, read_loss ? d_loss + 1 : nullptr));
       } else {
-        RMCHK(g.ctx, rm_sample_batch(g.ctx, d_org.f(), d_dir.f(), d_tgt.f(), P, d_fg.i(), n_fg_list, n_uni, n_boost,
-                                     cfg->seed, sample_stream, (uint64_t)global_step, b_org.f(), b_dir.f(), b_tgt.f(),
-                                     nullptr));
-        RMCHK(g.ctx, rm_train_step(g.ctx, b_org.f(), b_dir.f(), b_tgt.f(), n, progress, inv_count, &sc, &march, &gr,
-                                   d_loss, nullptr, 0));
+        // draw + render + backward (one launch for the small models), then the all-reduce
+        RMCHK(g.ctx, rm_train_step_sampled(g.ctx, d_org.f(), d_dir.f(), d_tgt.f(), P, d_fg.i(), n_fg_list, n_uni,
+                                           n_boost, cfg->seed, sample_stream, (uint64_t)global_step, progress,
+                                           inv_count, &sc, &march, &gr, d_loss));
         if (comm && (rc = comm->all_reduce_sum(comm->state, d_grad.f(), (int64_t)np + 1, g.stream)) != RMH_OK)
           return fail(rc, "all-reduce of the gradient (stage %d, step %d): %s", stage, step, rmh_last_error());
         // the penalty share of the loss costs a summation launch: only on the steps that report it

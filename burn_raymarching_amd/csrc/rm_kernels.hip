@@ -277,7 +277,7 @@ __host__ __device__ inline size_t tiles_offset(int npairs, int nprep) {
 // Then the escape thresholds of the march: kEscTab floats (see write_bound).
 constexpr int kEscTab = 64;
 constexpr int kStatsWords = 6;  // rm_stats device counters (KArgs::stats)
-constexpr int kDeadCountSlot = 44;  // Lds::misc int: the hand-off's count of waves that ended early
+[[maybe_unused]] constexpr int kDeadCountSlot = 44;  // Lds::misc int: the hand-off's count of waves that ended early
 __host__ __device__ inline size_t esc_offset(int npairs, int nprep) {
   const size_t nrb = (size_t)npairs / 8;
   return tiles_offset(npairs, nprep) + nrb * 64 * 16 + nrb * 32 * sizeof(float);
@@ -4023,7 +4023,7 @@ int run_small(rm_context* ctx, const Call& c, KArgs& a, long long n) {
       RM_HIP(ctx, hipMalloc(&ctx->btrace, sizeof(unsigned long long) * kTraceWords * kWaves * (size_t)kMaxBlocksPerLaunch));
     RM_HIP(ctx, hipMemsetAsync(ctx->btrace, 0, sizeof(unsigned long long) * kTraceWords * kWaves * (size_t)(nb + 1), ctx->stream));
     a.btrace = ctx->btrace;
-    ctx->btrace_waves = (nb + (c.fused ? 1 : 0)) * kWaves;
+    ctx->btrace_waves = (nb + (c.fused && c.fused->adam ? 1 : 0)) * kWaves;
 #endif
     SmallArgs sa;
     std::memset(&sa, 0, sizeof sa);
@@ -4032,19 +4032,20 @@ int run_small(rm_context* ctx, const Call& c, KArgs& a, long long n) {
     sa.arrivals = ctx->arrivals;
     sa.final_in_kernel = has_bwd && nb <= kSmallFinalMaxBlocks && !env_is("RM_SMALL_FINAL", '0') ? 1 : 0;
     sa.acquire = env_is("RM_SMALL_ACQUIRE", '0') ? 0 : 1;
-    if (c.fused && (!sa.final_in_kernel || nr != n))  // rm_train_iteration checked this
+    if (c.fused && (!sa.final_in_kernel || nr != n))  // rm_train_iteration / _step_sampled checked this
       return fail(ctx, RM_ERR_INVALID_ARG, "fused iteration needs one launch of <= %d blocks", kSmallFinalMaxBlocks);
+    const bool extra = c.fused && sa.adam;  // the launch's extra (optimizer) block
     if (ctx->stats_dev) {
       ctx->stats_blocks += nb;
       ctx->stats_waves += nb * kWaves;
     }
-    if (c.fused) {  // the extra block's optimizer part (rm_small.h)
+    if (extra) {  // the extra block's optimizer part (rm_small.h)
       if (!ctx->opt_pre) RM_HIP(ctx, hipMalloc(&ctx->opt_pre, sizeof(float) * (4 * kOptPreStride + 2)));
       sa.opt_pre = ctx->opt_pre;
     }
     hipEvent_t ev0, ev1;
     if ((rc = next_events(ctx, ev0, ev1)) != RM_OK) return rc;
-    const dim3 grid((unsigned)(nb + (c.fused ? 1 : 0)));
+    const dim3 grid((unsigned)(nb + (extra ? 1 : 0)));
     if (c.fused && lpr == 2) launch_small_m<kTrain, true, 2>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
     else if (c.fused) launch_small_m<kTrain, true>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
     else if (c.mode == kFwd) launch_small_m<kFwd>(a.M, grid, ctx->stream, a, sa, ev0, ev1);
@@ -4975,6 +4976,108 @@ int rm_train_step_camera_adam(rm_context* ctx, const rm_camera* cams, int32_t nu
                                with_penalties, loss_penalty, act_packed, colors_f16_out);
 }
 
+}  // extern "C"
+
+namespace {
+
+// rm_sample_batch into the context's batch buffer, then rm_train_step on it: the separate-call
+// form of the sampled step (rm_train_iteration's and rm_train_step_sampled's other sizes)
+int sample_then_train(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
+                      int64_t num_src, const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform, int64_t n_fg,
+                      uint64_t seed, uint64_t stream, uint64_t counter, float progress, float inv_count,
+                      const rm_scene* sc, const rm_march* march, const rm_grads* gr, float* loss_sum) {
+  const long long n = n_uniform + n_fg;
+  int rc;
+  if (n > 0) {
+    const size_t need = sizeof(float) * 9 * (size_t)n;
+    if (need > ctx->batch_bytes) {
+      if (ctx->batch) {
+        RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
+        RM_HIP(ctx, hipFree(ctx->batch));
+        ctx->batch = nullptr;
+        ctx->batch_bytes = 0;
+      }
+      if (hipMalloc(&ctx->batch, need) != hipSuccess) return fail(ctx, RM_ERR_OOM, "batch buffer (%zu B)", need);
+      ctx->batch_bytes = need;
+    }
+  }
+  float* bo = ctx->batch;
+  float* bd = bo ? bo + 3 * n : nullptr;
+  float* bt = bo ? bo + 6 * n : nullptr;
+  if (n > 0 && (rc = rm_sample_batch(ctx, ray_org, ray_dir, targets, num_src, fg_indices, num_fg, n_uniform, n_fg, seed,
+                                     stream, counter, bo, bd, bt, nullptr)) != RM_OK)
+    return rc;
+  return rm_train_step(ctx, bo, bd, bt, n, progress, inv_count, sc, march, gr, loss_sum, nullptr, 0);
+}
+
+// the sampled step's validation (rm_train_iteration and rm_train_step_sampled)
+int check_sampling(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
+                   int64_t num_src, const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform, int64_t n_fg) {
+  if (!ray_org || !ray_dir || !targets) return fail(ctx, RM_ERR_INVALID_ARG, "NULL dataset array");
+  if (num_src < 1 || num_src > INT32_MAX || n_uniform < 0 || n_fg < 0 || num_fg < 0)
+    return fail(ctx, RM_ERR_INVALID_ARG, "bad sampling sizes");
+  if (n_fg > 0 && (num_fg == 0 || !fg_indices)) return fail(ctx, RM_ERR_INVALID_ARG, "n_fg > 0 needs foreground indices");
+  return RM_OK;
+}
+
+// one launch of the small-scene kernel with its in-kernel final reduction for this call
+bool sampled_one_launch(const Call& c, int M, long long n) {
+  const int rpb = kBlock / small_lpr(c, n);
+  return use_small(c, M, n) && (n + rpb - 1) / rpb <= kSmallFinalMaxBlocks &&
+         (n + rpb - 1) / rpb <= max_blocks_per_launch() && !env_is("RM_SMALL_FINAL", '0') &&
+         !env_is("RM_FUSED_ITER", '0');
+}
+
+}  // namespace
+
+extern "C" {
+
+int rm_train_step_sampled(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
+                          int64_t num_src, const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform,
+                          int64_t n_fg, uint64_t seed, uint64_t stream, uint64_t counter, float progress,
+                          float inv_count, const rm_scene* scene, const rm_march* march, const rm_grads* grads,
+                          float* loss_sum) {
+  if (!ctx) return RM_ERR_INVALID_ARG;
+  int rc;
+  if ((rc = check_sampling(ctx, ray_org, ray_dir, targets, num_src, fg_indices, num_fg, n_uniform, n_fg)) != RM_OK)
+    return rc;
+  if (!scene || !march || !grads) return fail(ctx, RM_ERR_INVALID_ARG, "NULL scene / march / grads");
+  if (scene->num_spheres < 1 || scene->num_spheres > RM_MAX_SPHERES) return fail(ctx, RM_ERR_INVALID_ARG, "bad num_spheres");
+  const long long n = n_uniform + n_fg;
+  Call c;
+  c.mode = kTrain;
+  c.cam = false;
+  c.org = ray_org;
+  c.dir = ray_dir;
+  c.n = n;
+  c.targets = targets;
+  c.progress = progress;
+  c.inv_count = inv_count;
+  c.scene = scene;
+  c.march = march;
+  c.grads = grads;
+  c.loss_sum = loss_sum;
+  c.accumulate = 0;
+  // one launch: the small kernel draws its rays and reduces the gradient in its last block
+  if (n > 0 && sampled_one_launch(c, scene->num_spheres, n) && ctx->sdev == nullptr) {
+    SmallArgs fz;
+    std::memset(&fz, 0, sizeof fz);
+    fz.src_org = ray_org;
+    fz.src_dir = ray_dir;
+    fz.src_tgt = targets;
+    fz.fg = fg_indices;
+    fz.num_src = num_src;
+    fz.num_fg = num_fg;
+    fz.n_uniform = n_uniform;
+    fz.key = sample_key(seed, stream, counter);
+    fz.adam = 0;
+    c.fused = &fz;
+    return run(ctx, c);
+  }
+  return sample_then_train(ctx, ray_org, ray_dir, targets, num_src, fg_indices, num_fg, n_uniform, n_fg, seed, stream,
+                           counter, progress, inv_count, scene, march, grads, loss_sum);
+}
+
 int rm_train_iteration(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
                        int64_t num_src, const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform, int64_t n_fg,
                        uint64_t seed, uint64_t stream, uint64_t counter, float progress, float inv_count,
@@ -4982,15 +5085,14 @@ int rm_train_iteration(rm_context* ctx, const float* ray_org, const float* ray_d
                        float* adam_m, float* adam_v, int32_t num_spheres, int32_t step, float lr,
                        float weight_decay, int32_t with_penalties, float* loss_sum, float* loss_penalty) {
   if (!ctx) return RM_ERR_INVALID_ARG;
-  if (!ray_org || !ray_dir || !targets) return fail(ctx, RM_ERR_INVALID_ARG, "NULL dataset array");
+  int rc;
+  if ((rc = check_sampling(ctx, ray_org, ray_dir, targets, num_src, fg_indices, num_fg, n_uniform, n_fg)) != RM_OK)
+    return rc;
   if (!act_packed || !grad_packed || !raw_packed || !adam_m || !adam_v || !march)
     return fail(ctx, RM_ERR_INVALID_ARG, "NULL model buffer");
   if (num_spheres < 1 || num_spheres > RM_MAX_SPHERES) return fail(ctx, RM_ERR_INVALID_ARG, "bad num_spheres");
   if ((march->flags & RM_MARCH_COLOR_F16) != 0)
     return fail(ctx, RM_ERR_INVALID_ARG, "rm_train_iteration trains fp32 colour models");
-  if (num_src < 1 || num_src > INT32_MAX || n_uniform < 0 || n_fg < 0 || num_fg < 0)
-    return fail(ctx, RM_ERR_INVALID_ARG, "bad sampling sizes");
-  if (n_fg > 0 && (num_fg == 0 || !fg_indices)) return fail(ctx, RM_ERR_INVALID_ARG, "n_fg > 0 needs foreground indices");
   if (step < 1 && !ctx->sdev) return fail(ctx, RM_ERR_INVALID_ARG, "step counts from 1");
   const int M = num_spheres;
   const long long n = n_uniform + n_fg;
@@ -5013,11 +5115,7 @@ int rm_train_iteration(rm_context* ctx, const float* ray_org, const float* ray_d
   c.loss_sum = loss_sum;
   c.accumulate = 0;
   // one launch: the small kernel with its in-kernel final reduction (RM_FUSED_ITER=0: three calls)
-  const int rpb = kBlock / small_lpr(c, n);
-  const bool fused = use_small(c, M, n) && (n + rpb - 1) / rpb <= kSmallFinalMaxBlocks &&
-                     (n + rpb - 1) / rpb <= max_blocks_per_launch() &&
-                     M <= kOptSmallMaxM && !env_is("RM_SMALL_FINAL", '0') &&
-                     !env_is("RM_FUSED_ITER", '0') && ctx->sdev == nullptr;
+  const bool fused = sampled_one_launch(c, M, n) && M <= kOptSmallMaxM && ctx->sdev == nullptr;
   if (fused) {
     SmallArgs fz;
     std::memset(&fz, 0, sizeof fz);
@@ -5038,31 +5136,13 @@ int rm_train_iteration(rm_context* ctx, const float* ray_org, const float* ray_d
     fz.wd = weight_decay;
     fz.loss_penalty = loss_penalty;
     fz.act_out = act_packed;
+    fz.adam = 1;
     c.fused = &fz;
     return run(ctx, c);
   }
   // the same three steps as separate calls: draw + gather, train step, optimizer
-  int rc;
-  if (n > 0) {
-    const size_t need = sizeof(float) * 9 * (size_t)n;
-    if (need > ctx->batch_bytes) {
-      if (ctx->batch) {
-        RM_HIP(ctx, hipStreamSynchronize(ctx->stream));
-        RM_HIP(ctx, hipFree(ctx->batch));
-        ctx->batch = nullptr;
-        ctx->batch_bytes = 0;
-      }
-      if (hipMalloc(&ctx->batch, need) != hipSuccess) return fail(ctx, RM_ERR_OOM, "batch buffer (%zu B)", need);
-      ctx->batch_bytes = need;
-    }
-  }
-  float* bo = ctx->batch;
-  float* bd = bo ? bo + 3 * n : nullptr;
-  float* bt = bo ? bo + 6 * n : nullptr;
-  if (n > 0 && (rc = rm_sample_batch(ctx, ray_org, ray_dir, targets, num_src, fg_indices, num_fg, n_uniform, n_fg, seed,
-                                     stream, counter, bo, bd, bt, nullptr)) != RM_OK)
-    return rc;
-  if ((rc = rm_train_step(ctx, bo, bd, bt, n, progress, inv_count, &sc, march, &gr, loss_sum, nullptr, 0)) != RM_OK)
+  if ((rc = sample_then_train(ctx, ray_org, ray_dir, targets, num_src, fg_indices, num_fg, n_uniform, n_fg, seed,
+                              stream, counter, progress, inv_count, &sc, march, &gr, loss_sum)) != RM_OK)
     return rc;
   return rm_optimizer_step(ctx, raw_packed, grad_packed, adam_m, adam_v, M, step, lr, weight_decay, with_penalties,
                            loss_penalty, act_packed);

@@ -23,10 +23,15 @@
 //    wave with the transposing 8-value reduction (wave_reduce8), the four waves in LDS in order.
 // Deterministic: every sum has a fixed order (lanes, waves, blocks).
 // FUSED (rm_train_iteration): the reference loop's whole step in this one launch -- the batch drawn
-// and gathered per ray, and the optimizer step run by the last block after the gradient sums.
+// and gathered per ray, and the optimizer step run by the last block after the gradient sums;
+// with sa.adam = 0 (rm_train_step_sampled, the data-parallel step) the draw, render and gradient
+// only, the optimizer left for after the all-reduce.
 #pragma once
 
 constexpr int kSmallMaxM = 32;             // spheres handled by the small kernel
+#ifndef RM_SMALL_FIN_PAIRS
+#define RM_SMALL_FIN_PAIRS 0  // 1: the final block sums the records' columns two at a time (8-byte loads; measured equal)
+#endif
 #ifndef RM_SMALL_FIN_BATCH
 #define RM_SMALL_FIN_BATCH 32  // record rows in flight per thread in the final block's sums
 #endif
@@ -55,6 +60,8 @@ struct SmallArgs {
   float* act_out;         // the next render's activated parameters (the scene this launch read)
   float* opt_pre;         // FUSED: [4][kOptPreStride] chain-rule factor and penalty terms per element,
                           // then Adam's two bias corrections (the extra block -> the final block)
+  int adam;               // FUSED: 1 -- the extra block and the optimizer step (rm_train_iteration);
+                          // 0 -- the drawn batch's gradient only, for an all-reduce (rm_train_step_sampled)
 };
 constexpr int kOptPreStride = 256;  // >= 7 kSmallMaxM + 4 elements
 static_assert(7 * kSmallMaxM + 4 <= kOptPreStride, "one opt_pre column per element");
@@ -160,7 +167,9 @@ __device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa,
   auto col_of = [&](int idx) { return idx < M * 8 ? idx : Mpad * 8 + (idx - M * 8); };
   // FUSED: the optimizer's parameters and moments load while the block sums the records
   OptPrefetch pf;
-  if constexpr (FUSED) pf = opt_prefetch(sa.raw, sa.m1, sa.m2, M);
+  if constexpr (FUSED) {
+    if (sa.adam) pf = opt_prefetch(sa.raw, sa.m1, sa.m2, M);
+  }
   // The records are read with write-through-cache (sc1) loads only, stored sc1 by every block,
   // each storing wave drained (vmcnt(0)) before the barrier behind which one lane adds to the one
   // counter whose last add tells this block: the hand-off row of MI355X_MICROARCH.md
@@ -175,7 +184,7 @@ __device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa,
   RM_TRACE(11, __builtin_amdgcn_s_memrealtime());
   // FUSED: the extra block's optimizer part, loaded with the records (the same hand-off)
   [[maybe_unused]] OptPre opre;
-  if constexpr (FUSED) {
+  if (FUSED && sa.adam) {
     const int n = 7 * M + 4;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -196,6 +205,36 @@ __device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa,
   // launch of up to kSmallFinalMaxBlocks blocks takes one or two rounds.
   constexpr int kFinBatch = RM_SMALL_FIN_BATCH;
   const int nb = nrows;
+#if RM_SMALL_FIN_PAIRS
+  // the columns two at a time (8-byte sc1 loads; a pair never straddles the gap between the
+  // spheres' M*8 columns and the scalars), so that twice the chains fit the block: at 128 records
+  // a thread's rows take one round of loads instead of two
+  const int npair = nneed / 2;
+  const int chains = max(1, min(16, kBlock / npair));
+  for (int w = tid; w < npair * chains; w += kBlock) {
+    const int pi = w % npair, ch = w / npair;
+    const long long e = col_of(2 * pi);
+    float acc0 = 0.0f, acc1 = 0.0f;
+    for (int b0 = ch; b0 < nb; b0 += kFinBatch * chains) {
+      unsigned long long v[kFinBatch];
+#pragma unroll
+      for (int u = 0; u < kFinBatch; ++u) {
+        const int b = b0 + u * chains;
+        v[u] = b < nb ? __hip_atomic_load(reinterpret_cast<const unsigned long long*>(a.partials + (long long)b * a.rec + e),
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : 0ull;
+      }
+#pragma unroll
+      for (int u = 0; u < kFinBatch; ++u)
+        if (b0 + u * chains < nb) {
+          acc0 += __uint_as_float((unsigned)(v[u] & 0xFFFFFFFFull));
+          acc1 += __uint_as_float((unsigned)(v[u] >> 32));
+        }
+    }
+    s_red[ch * nneed + 2 * pi] = acc0;
+    s_red[ch * nneed + 2 * pi + 1] = acc1;
+  }
+#else
   const int chains = max(1, min(8, kBlock / nneed));
   for (int w = tid; w < nneed * chains; w += kBlock) {
     const int idx = w % nneed, ch = w / nneed;
@@ -216,6 +255,7 @@ __device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa,
     }
     s_red[ch * nneed + idx] = acc;
   }
+#endif
   __syncthreads();
   RM_TRACE(2, __builtin_amdgcn_s_memrealtime());
   const FinalArgs& f = sa.fin;
@@ -260,7 +300,7 @@ __device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa,
   }
   RM_TRACE(9, __builtin_amdgcn_s_memrealtime());
   RM_TRACE(1, __builtin_amdgcn_s_memrealtime());
-  if constexpr (FUSED) {
+  if (FUSED && sa.adam) {
     // the optimizer step (rm_optimizer_step: penalties + Adam, train.rs:198) on the gradient just
     // summed (its LDS copy in the packed layout). Every other block has arrived, so nothing reads
     // the activated or raw parameters any more when act_out and raw are overwritten.
@@ -305,7 +345,7 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
     // repulsion rows, chain-rule factors, penalty terms and loss, Adam's bias corrections) on a CU
     // of its own while the ray blocks run, handed to the final block through sa.opt_pre
     // (write-through stores before the arrival, as the records)
-    if (blockIdx.x == gridDim.x - 1) {
+    if (sa.adam && blockIdx.x == gridDim.x - 1) {
       const OptPrefetch pf = opt_prefetch(sa.raw, sa.m1, sa.m2, M);
       const OptPre o = opt_small_pre(pf, M, sa.step, sa.with_pen, sa.loss_penalty);
       const int n = 7 * M + 4;
@@ -650,5 +690,5 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
   RM_TRACE(8, __builtin_amdgcn_s_memrealtime());
   RM_TRACE(1, __builtin_amdgcn_s_memrealtime());
   if (!last) return;
-  small_final<FUSED>(a, sa, FUSED ? (int)gridDim.x - 1 : (int)gridDim.x, s_red, ldn, ldlen);
+  small_final<FUSED>(a, sa, FUSED && sa.adam ? (int)gridDim.x - 1 : (int)gridDim.x, s_red, ldn, ldlen);
 }

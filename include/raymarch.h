@@ -376,6 +376,21 @@ int rm_train_step_camera_adam(rm_context* ctx, const rm_camera* cams, int32_t nu
  * gradient-independent part beside the ray blocks and the last block applies the update; env
  * RM_FUSED_ITER=0 turns this off); other sizes run the three calls. fp32 colour models only.
  * Not for data-parallel training: the gradient is consumed before it could be all-reduced. */
+/* The data-parallel rank's step before its all-reduce (train.rs:179-190 on the rank's share of
+ * the batch), replacing the sequence rm_sample_batch -> rm_train_step with the same arguments and
+ * the same results bit for bit: the rows drawn from the dataset arrays as rm_sample_batch draws
+ * them (n_uniform + n_fg rows; seed, stream, counter), then the render of `scene`, the loss seed
+ * and the backward into `grads` and loss_sum (overwritten), as rm_train_step with progress,
+ * inv_count and march (accumulate 0, no per-ray output). The gradient is left for the caller's
+ * all-reduce and rm_optimizer_step[_f16]. Models of up to 32 spheres and batches of up to 16,384
+ * rays run as ONE launch (the small-scene kernel draws and gathers its rays and its last block
+ * completes the gradient; env RM_FUSED_ITER=0 turns this off); other sizes run the two calls. */
+int rm_train_step_sampled(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
+                          int64_t num_src, const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform,
+                          int64_t n_fg, uint64_t seed, uint64_t stream, uint64_t counter, float progress,
+                          float inv_count, const rm_scene* scene, const rm_march* march, const rm_grads* grads,
+                          float* loss_sum);
+
 int rm_train_iteration(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
                        int64_t num_src, const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform, int64_t n_fg,
                        uint64_t seed, uint64_t stream, uint64_t counter, float progress, float inv_count,

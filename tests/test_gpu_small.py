@@ -233,9 +233,11 @@ def test_small_and_general_kernel_agree(rm, oracle, monkeypatch):
 
 def _iteration(torch, native, render, model, src, fg, nu, nf, sc, steps, fused, monkeypatch):
     """`steps` training iterations (train.rs:169-198) through rm_train_iteration (fused: one launch
-    when eligible) or through rm_sample_batch + rm_train_step + rm_optimizer_step."""
+    when eligible), through rm_sample_batch + rm_train_step + rm_optimizer_step (fused False), or
+    through rm_train_step_sampled + rm_optimizer_step (fused "sampled": a data-parallel rank's
+    calls around its all-reduce)."""
     import ctypes
-    monkeypatch.setenv("RM_FUSED_ITER", "1" if fused else "0")
+    monkeypatch.setenv("RM_FUSED_ITER", "0" if fused is False else "1")
     m = sc["centers"].shape[0]
     sm = model.SceneModel.from_activated(sc["centers"], sc["colors"], sc["radius"], sc["light_dir"], sc["ambient"])
     raw = sm.raw.clone()
@@ -253,7 +255,17 @@ def _iteration(torch, native, render, model, src, fg, nu, nf, sc, steps, fused, 
         k = 5.0 + 27.0 * it / steps
         march = native.march_params(40, k)
         args = (o.shape[0], p(fg), fg.numel(), nu, nf, 11, 1, it, it / steps, 1.0 / (3 * n))
-        if fused:
+        if fused == "sampled":
+            s = native.RmScene()
+            ctx._lib.rm_scene_from_packed(p(act), m, ctypes.byref(s))
+            g = native.RmGrads()
+            ctx._lib.rm_grads_from_packed(p(grad), m, ctypes.byref(g))
+            ctx.check(ctx._lib.rm_train_step_sampled(ctx.handle, p(o), p(d), p(t), *args, ctypes.byref(s),
+                                                     ctypes.byref(march), ctypes.byref(g), p(loss)),
+                      "rm_train_step_sampled")
+            ctx.check(ctx._lib.rm_optimizer_step(ctx.handle, p(raw), p(grad), p(mom[0]), p(mom[1]), m, it, 0.01, 1e-5, 1,
+                                                 ctypes.c_void_p(loss.data_ptr() + 4), p(act)), "rm_optimizer_step")
+        elif fused:
             ctx.check(ctx._lib.rm_train_iteration(ctx.handle, p(o), p(d), p(t), *args, ctypes.byref(march), p(act),
                                                   p(grad), p(raw), p(mom[0]), p(mom[1]), m, it, 0.01, 1e-5, 1,
                                                   p(loss), ctypes.c_void_p(loss.data_ptr() + 4)), "rm_train_iteration")
@@ -300,3 +312,28 @@ def test_train_iteration_equals_three_calls(rm, oracle, monkeypatch, m, nu, nf):
         for name, u, v in zip(names, xa, xb):
             assert torch.equal(u, v), (it, name, (u - v).abs().max().item())
     assert torch.isfinite(a[-1][0]).all() and a[-1][5][0] > 0
+
+
+@pytest.mark.parametrize("m,nu,nf", [(7, 13107, 3277), (32, 9000, 7384), (40, 13107, 3277), (9, 40000, 0)])
+def test_train_step_sampled_equals_two_calls(rm, oracle, monkeypatch, m, nu, nf):
+    """rm_train_step_sampled = rm_sample_batch -> rm_train_step, bit for bit (the gradient, the loss
+    and, through the optimizer after it, the parameters), over five iterations with k annealed:
+    the data-parallel rank's step before its all-reduce. One launch (the small kernel without its
+    optimizer block) for M <= 32 and <= 16,384 rays; M = 40 and 40,000 rays run the two calls."""
+    import torch
+    render, model, native = rm
+    cams = model.ring_cameras(4)
+    rays = [oracle.camera_rays(64, 64, *c, precision="f32") for c in cams]
+    o = np.concatenate([r[0] for r in rays])
+    d = np.concatenate([r[1] for r in rays])
+    tg = oracle.render_diff(o.astype(np.float64), d.astype(np.float64), train_scene(model, 6, 2), 24, 32.0)
+    src = [dev(o), dev(d), dev(tg)]
+    fg = torch.from_numpy(np.flatnonzero(tg.sum(1) > 0.01).astype(np.int32)).cuda()
+    sc = train_scene(model, m, 60 + m)
+    a = _iteration(torch, native, render, model, src, fg, nu, nf, sc, 5, "sampled", monkeypatch)
+    b = _iteration(torch, native, render, model, src, fg, nu, nf, sc, 5, False, monkeypatch)
+    names = ("raw", "act", "grad", "adam_m", "adam_v", "loss")
+    for it, (xa, xb) in enumerate(zip(a, b)):
+        for name, u, v in zip(names, xa, xb):
+            assert torch.equal(u, v), (it, name, (u - v).abs().max().item())
+    assert torch.isfinite(a[-1][2]).all() and a[-1][5][0] > 0
