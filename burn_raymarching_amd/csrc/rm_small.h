@@ -29,9 +29,6 @@
 #pragma once
 
 constexpr int kSmallMaxM = 32;             // spheres handled by the small kernel
-#ifndef RM_SMALL_FIN_PAIRS
-#define RM_SMALL_FIN_PAIRS 0  // 1: the final block sums the records' columns two at a time (8-byte loads; measured equal)
-#endif
 #ifndef RM_SMALL_FIN_BATCH
 #define RM_SMALL_FIN_BATCH 32  // record rows in flight per thread in the final block's sums
 #endif
@@ -205,49 +202,28 @@ __device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa,
   // launch of up to kSmallFinalMaxBlocks blocks takes one or two rounds.
   constexpr int kFinBatch = RM_SMALL_FIN_BATCH;
   const int nb = nrows;
-#if RM_SMALL_FIN_PAIRS
-  // the columns two at a time (8-byte sc1 loads; a pair never straddles the gap between the
-  // spheres' M*8 columns and the scalars), so that twice the chains fit the block: at 128 records
-  // a thread's rows take one round of loads instead of two
-  const int npair = nneed / 2;
-  const int chains = max(1, min(16, kBlock / npair));
-  for (int w = tid; w < npair * chains; w += kBlock) {
-    const int pi = w % npair, ch = w / npair;
-    const long long e = col_of(2 * pi);
-    float acc0 = 0.0f, acc1 = 0.0f;
-    for (int b0 = ch; b0 < nb; b0 += kFinBatch * chains) {
-      unsigned long long v[kFinBatch];
-#pragma unroll
-      for (int u = 0; u < kFinBatch; ++u) {
-        const int b = b0 + u * chains;
-        v[u] = b < nb ? __hip_atomic_load(reinterpret_cast<const unsigned long long*>(a.partials + (long long)b * a.rec + e),
-                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                      : 0ull;
-      }
-#pragma unroll
-      for (int u = 0; u < kFinBatch; ++u)
-        if (b0 + u * chains < nb) {
-          acc0 += __uint_as_float((unsigned)(v[u] & 0xFFFFFFFFull));
-          acc1 += __uint_as_float((unsigned)(v[u] >> 32));
-        }
-    }
-    s_red[ch * nneed + 2 * pi] = acc0;
-    s_red[ch * nneed + 2 * pi + 1] = acc1;
-  }
-#else
+  // A load's address is a 32-bit byte offset from the records' base (saddr form), clamped into
+  // the last record instead of branching around the load (a launch's records are
+  // nb * rec <= 128 * 264 floats; a clamped row's value is dropped below): three full-rate
+  // instructions per load instead of a 64-bit multiply, quarter-rate integer multiplies and an
+  // exec-mask branch around each (issuing a thread's 32 loads was part of the sums' critical path)
   const int chains = max(1, min(8, kBlock / nneed));
+  const int rec32 = (int)a.rec;
+  const int stride = chains * rec32;  // one row of a chain to its next
+  const int last_row = (nb - 1) * rec32;
+  const char* pbytes = reinterpret_cast<const char*>(a.partials);
   for (int w = tid; w < nneed * chains; w += kBlock) {
     const int idx = w % nneed, ch = w / nneed;
-    const long long e = col_of(idx);
+    const int e = (int)col_of(idx);
     float acc = 0.0f;
     for (int b0 = ch; b0 < nb; b0 += kFinBatch * chains) {
+      const unsigned off0 = (unsigned)(b0 * rec32 + e);
       float v[kFinBatch];
 #pragma unroll
       for (int u = 0; u < kFinBatch; ++u) {
-        const int b = b0 + u * chains;
-        v[u] = b < nb ? __hip_atomic_load(a.partials + (long long)b * a.rec + e, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT)
-                      : 0.0f;
+        const unsigned off = min(off0 + (unsigned)(u * stride), (unsigned)(last_row + e));  // floats
+        v[u] = __hip_atomic_load(reinterpret_cast<const float*>(pbytes + 4u * off), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
       }
 #pragma unroll
       for (int u = 0; u < kFinBatch; ++u)
@@ -255,7 +231,6 @@ __device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa,
     }
     s_red[ch * nneed + idx] = acc;
   }
-#endif
   __syncthreads();
   RM_TRACE(2, __builtin_amdgcn_s_memrealtime());
   const FinalArgs& f = sa.fin;
