@@ -1,10 +1,10 @@
 #!/bin/bash
-# Round 5: the small kernel's final-block record sums with 32-bit clamped offsets (three full-rate
-# instructions per load, no branch) against HEAD's 64-bit addressing (lib/var/finhead.so): the
-# small-kernel tests, then rm_train (one process and --ranks 1) A B A B A B on one box.
+# Round 5: small-kernel final-block A/B: the working tree against lib/var/finhead.so (built from the
+# previous revision by tools/build_variant.sh; r06aa: 32-bit clamped load offsets, r06ac: one load round
+# at M = 9): the small-kernel tests, then rm_train (one process and --ranks 1) A B A B A B on one box.
 set -o pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r06aa
+O=gpurun_out/${TAG:-r06aa}
 mkdir -p $O/train_out
 L=burn_raymarching_amd/lib
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_small.py \
