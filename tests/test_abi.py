@@ -67,6 +67,11 @@ def test_null_context_is_rejected(native):
     assert lib.rm_render_diff(None, None, None, 0, None, None, None, None) == 1  # RM_ERR_INVALID_ARG
     assert lib.rm_last_error(None) == b"NULL context"
     assert lib.rm_create(0, None, None) == 1
+    # the sampled steps (rm_train_step_sampled, rm_train_iteration) check the context first
+    assert lib.rm_train_step_sampled(None, None, None, None, 1, None, 0, 0, 0, 0, 0, 0, 0.0, 1.0, None, None, None,
+                                     None) == 1
+    assert lib.rm_train_iteration(None, None, None, None, 1, None, 0, 0, 0, 0, 0, 0, 0.0, 1.0, None, None, None, None,
+                                  None, None, 1, 1, 0.01, 0.0, 0, None, None) == 1
 
 
 def test_packed_views(native):

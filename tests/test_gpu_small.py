@@ -337,3 +337,41 @@ def test_train_step_sampled_equals_two_calls(rm, oracle, monkeypatch, m, nu, nf)
         for name, u, v in zip(names, xa, xb):
             assert torch.equal(u, v), (it, name, (u - v).abs().max().item())
     assert torch.isfinite(a[-1][2]).all() and a[-1][5][0] > 0
+
+
+def test_train_step_sampled_arguments_and_empty_batch(rm):
+    """rm_train_step_sampled's argument checks (dataset arrays, sampling sizes, foreground list,
+    scene / march / grads: RM_ERR_INVALID_ARG, nothing launched) and an empty batch (no rays: the
+    gradient and the loss sum are written as zeros, as rm_train_step with no rays writes them)."""
+    import ctypes
+    import torch
+    render, model, native = rm
+    ctx = render.context()
+    lib = ctx._lib
+    p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    m = 7
+    src = torch.rand(64, 3, device="cuda")
+    fg = torch.arange(8, dtype=torch.int32, device="cuda")
+    act = torch.rand(model.packed_size(m), device="cuda")
+    grad = torch.full((model.packed_size(m),), 7.0, device="cuda")
+    loss = torch.full((1,), 7.0, device="cuda")
+    s = native.RmScene()
+    lib.rm_scene_from_packed(p(act), m, ctypes.byref(s))
+    g = native.RmGrads()
+    lib.rm_grads_from_packed(p(grad), m, ctypes.byref(g))
+    march = native.march_params(16, 32.0)
+
+    def call(o, d, t, num_src, fgp, num_fg, nu, nf, scene=ctypes.byref(s), mp=ctypes.byref(march), gp=ctypes.byref(g)):
+        return lib.rm_train_step_sampled(ctx.handle, o, d, t, num_src, fgp, num_fg, nu, nf, 1, 1, 1, 0.5, 1.0 / 3,
+                                         scene, mp, gp, p(loss))
+    assert call(None, p(src), p(src), 64, None, 0, 8, 0) == 1  # NULL dataset array
+    assert call(p(src), p(src), p(src), 0, None, 0, 8, 0) == 1  # no source rows
+    assert call(p(src), p(src), p(src), 64, None, 0, 8, -1) == 1  # negative count
+    assert call(p(src), p(src), p(src), 64, None, 0, 4, 4) == 1  # n_fg > 0 without foreground indices
+    assert call(p(src), p(src), p(src), 64, p(fg), 8, 4, 4, scene=None) == 1
+    assert call(p(src), p(src), p(src), 64, p(fg), 8, 4, 4, gp=None) == 1
+    torch.cuda.synchronize()
+    assert torch.all(grad == 7.0) and loss.item() == 7.0  # nothing ran
+    ctx.check(call(p(src), p(src), p(src), 64, p(fg), 8, 0, 0), "rm_train_step_sampled (empty)")
+    torch.cuda.synchronize()
+    assert torch.all(grad == 0.0) and loss.item() == 0.0
