@@ -375,3 +375,54 @@ def test_train_step_sampled_arguments_and_empty_batch(rm):
     ctx.check(call(p(src), p(src), p(src), 64, p(fg), 8, 0, 0), "rm_train_step_sampled (empty)")
     torch.cuda.synchronize()
     assert torch.all(grad == 0.0) and loss.item() == 0.0
+
+
+@pytest.mark.parametrize("m", [7, 24])
+def test_train_step_sampled_color_f16(rm, oracle, m):
+    """An fp16-colour model (RM_MARCH_COLOR_F16: the scene's colours are halves) through
+    rm_train_step_sampled -- the multi-rank driver's step for every model, the fp16 growth runs
+    included -- equals rm_sample_batch + rm_train_step bit for bit (gradient and loss sum)."""
+    import ctypes
+    import torch
+    render, model, native = rm
+    ctx = render.context()
+    lib = ctx._lib
+    p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    cams = model.ring_cameras(3)
+    rays = [oracle.camera_rays(48, 48, *c, precision="f32") for c in cams]
+    o = dev(np.concatenate([r[0] for r in rays]))
+    d = dev(np.concatenate([r[1] for r in rays]))
+    tg = dev(np.random.default_rng(m).uniform(size=(o.shape[0], 3)))
+    fg = torch.arange(0, o.shape[0], 3, dtype=torch.int32, device="cuda")
+    sc = train_scene(model, m, 70 + m)
+    act = model.SceneModel.from_activated(sc["centers"], sc["colors"], sc["radius"], sc["light_dir"],
+                                          sc["ambient"]).activated_packed().clone()
+    col_h = act[3 * m:6 * m].half().contiguous()
+    s = native.RmScene()
+    lib.rm_scene_from_packed(p(act), m, ctypes.byref(s))
+    s.colors = col_h.data_ptr()
+    march = native.march_params(40, 20.0)
+    march.flags |= native.RM_MARCH_COLOR_F16
+    nu, nf = 5000, 1500
+    out = []
+    for sampled in (True, False):
+        grad = torch.zeros(model.packed_size(m), device="cuda")
+        loss = torch.zeros(1, device="cuda")
+        g = native.RmGrads()
+        lib.rm_grads_from_packed(p(grad), m, ctypes.byref(g))
+        args = (o.shape[0], p(fg), fg.numel(), nu, nf, 5, 2, 9)
+        if sampled:
+            ctx.check(lib.rm_train_step_sampled(ctx.handle, p(o), p(d), p(tg), *args, 0.4, 1.0 / (3 * (nu + nf)),
+                                                ctypes.byref(s), ctypes.byref(march), ctypes.byref(g), p(loss)),
+                      "rm_train_step_sampled")
+        else:
+            b = [torch.empty((nu + nf, 3), device="cuda") for _ in range(3)]
+            ctx.check(lib.rm_sample_batch(ctx.handle, p(o), p(d), p(tg), *args, p(b[0]), p(b[1]), p(b[2]), None),
+                      "rm_sample_batch")
+            ctx.check(lib.rm_train_step(ctx.handle, p(b[0]), p(b[1]), p(b[2]), nu + nf, 0.4, 1.0 / (3 * (nu + nf)),
+                                        ctypes.byref(s), ctypes.byref(march), ctypes.byref(g), p(loss), None, 0),
+                      "rm_train_step")
+        torch.cuda.synchronize()
+        out.append((grad.clone(), loss.clone()))
+    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    assert torch.isfinite(out[0][0]).all() and out[0][1].item() > 0
