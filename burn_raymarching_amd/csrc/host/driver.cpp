@@ -30,6 +30,16 @@ namespace {
   } while (0)
 
 // Device buffer owned by the host driver.
+// Page-locked host memory (the loss readback: an async copy the stream wait then covers)
+struct PinnedBuf {
+  void* p = nullptr;
+  ~PinnedBuf() {
+    if (p) (void)hipHostFree(p);
+  }
+  hipError_t alloc(size_t n) { return hipHostMalloc(&p, n, hipHostMallocDefault); }
+  float* f() const { return (float*)p; }
+};
+
 struct DevBuf {
   void* p = nullptr;
   size_t bytes = 0;
@@ -291,6 +301,8 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
   rm_march_default(&march);
   march.steps = cfg->march_steps;
   if (f16) march.flags |= RM_MARCH_COLOR_F16;
+  PinnedBuf h_loss;  // the loss sum and penalty read back on reporting steps
+  HIPCHK(h_loss.alloc(2 * sizeof(float)));
   if (verbose) std::printf("Start Multi-Stage Optimization...\n");
 
   for (int32_t stage = 0; stage < cfg->stages; ++stage) {
@@ -382,17 +394,23 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
       if (comm && world > 1 && !read_loss && step % kStepsInFlight == 0 && (rc = sync_stream(g, comm)) != RMH_OK)
         return rc;
       if (read_loss) {
-        float s[2];
-        // drain the stream under the watchdog first: a copy to pageable memory blocks unguarded
+        // into page-locked memory on the stream, then one wait under the watchdog
+        HIPCHK(hipMemcpyAsync(h_loss.p, d_loss, 2 * sizeof(float), hipMemcpyDeviceToHost, g.stream));
         if ((rc = sync_stream(g, comm)) != RMH_OK) return rc;
-        HIPCHK(hipMemcpy(s, d_loss, sizeof s, hipMemcpyDeviceToHost));
+        const float* s = h_loss.f();
         last_loss = s[0] * inv_count + s[1];  // training.rs:34 + penalties
         if (verbose && step % cfg->log_every == 0)
           std::printf("  Step %d | Loss: %.5f | k: %.1f\n", step, last_loss, march.smooth_k);
       }
     }
+    const auto t_enq = std::chrono::steady_clock::now();  // the host has issued the stage's steps
     if ((rc = sync_stream(g, comm)) != RMH_OK) return rc;
-    seconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const auto t_end = std::chrono::steady_clock::now();
+    seconds += std::chrono::duration<double>(t_end - t0).count();
+    if (const char* e = std::getenv("RMH_STAGE_TIMES"); e && e[0] == '1')  // measurement: host issue vs drain
+      std::fprintf(stderr, "stage %d: issued in %.3f ms, drained %.3f ms later\n", stage + 1,
+                   1e3 * std::chrono::duration<double>(t_enq - t0).count(),
+                   1e3 * std::chrono::duration<double>(t_end - t_enq).count());
     HIPCHK(hipMemcpy(raw.data(), d_raw.p, sizeof(float) * np, hipMemcpyDeviceToHost));
     if (cfg->on_generation) cfg->on_generation(cfg->user, stage, M, raw.data());
 

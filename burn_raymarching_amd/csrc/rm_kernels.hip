@@ -4625,6 +4625,21 @@ int rm_reserve(rm_context* ctx, int64_t max_rays, int32_t max_spheres) {
   if (!ctx) return RM_ERR_INVALID_ARG;
   if (max_rays < 0 || max_spheres < 1 || max_spheres > RM_MAX_SPHERES)
     return fail(ctx, RM_ERR_INVALID_ARG, "bad reserve sizes");
+  // the small buffers the calls otherwise allocate on first use: the arrival counters of the
+  // in-kernel reductions (zeroed) and the fused iteration's optimizer hand-off
+  if (!ctx->arrivals) {
+    RM_HIP(ctx, hipMalloc(&ctx->arrivals, 64));
+    RM_HIP(ctx, hipMemsetAsync(ctx->arrivals, 0, 64, ctx->stream));
+  }
+  if (!ctx->red_arrivals) {
+    RM_HIP(ctx, hipMalloc(&ctx->red_arrivals, sizeof(unsigned) * kRedArrivals));
+    RM_HIP(ctx, hipMemsetAsync(ctx->red_arrivals, 0, sizeof(unsigned) * kRedArrivals, ctx->stream));
+  }
+  if (!ctx->opt_arrival) {
+    RM_HIP(ctx, hipMalloc(&ctx->opt_arrival, 128));
+    RM_HIP(ctx, hipMemsetAsync(ctx->opt_arrival, 0, 128, ctx->stream));
+  }
+  if (!ctx->opt_pre) RM_HIP(ctx, hipMalloc(&ctx->opt_pre, sizeof(float) * (4 * kOptPreStride + 2)));
   return ensure_ws(ctx, ws_need(std::max<int64_t>(max_rays, 1), max_spheres));
 }
 

@@ -159,7 +159,9 @@ void rm_destroy(rm_context* ctx);
 const char* rm_last_error(const rm_context* ctx);
 void rm_march_default(rm_march* m);
 /* Pre-size the workspace for backward/train calls of up to max_rays rays and
- * max_spheres spheres so later calls never allocate (needed for hipGraph capture). */
+ * max_spheres spheres, and allocate the context's small per-call buffers (reduction arrival
+ * counters, the fused iteration's optimizer hand-off), so later calls never allocate (needed
+ * for hipGraph capture; keeps first-call allocations out of a timed loop). */
 int rm_reserve(rm_context* ctx, int64_t max_rays, int32_t max_spheres);
 
 /* ---- forward: renderer_diff.rs:6-91 --------------------------------------- */
