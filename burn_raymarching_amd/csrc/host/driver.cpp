@@ -371,10 +371,12 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
                                         d_act.f(), d_grad.f(), d_raw.f(), d_m.f(), d_v.f(), M, step, (float)lr,
                                         cfg->weight_decay, 1, d_loss, read_loss ? d_loss + 1 : nullptr));
       } else {
-        // draw + render + backward (one launch for the small models), then the all-reduce
-        RMCHK(g.ctx, rm_train_step_sampled(g.ctx, d_org.f(), d_dir.f(), d_tgt.f(), P, d_fg.i(), n_fg_list, n_uni,
-                                           n_boost, cfg->seed, sample_stream, (uint64_t)global_step, progress,
-                                           inv_count, &sc, &march, &gr, d_loss));
+        // draw + render + backward (one launch for the small models, whose extra block also runs
+        // the optimizer's gradient-independent part), then the all-reduce, then the update
+        RMCHK(g.ctx, rm_train_step_sampled_prepared(g.ctx, d_org.f(), d_dir.f(), d_tgt.f(), P, d_fg.i(), n_fg_list,
+                                                    n_uni, n_boost, cfg->seed, sample_stream, (uint64_t)global_step,
+                                                    progress, inv_count, &sc, &march, &gr, d_loss, d_raw.f(), step, 1,
+                                                    read_loss ? d_loss + 1 : nullptr));
         if (comm && (rc = comm->all_reduce_sum(comm->state, d_grad.f(), (int64_t)np + 1, g.stream)) != RMH_OK)
           return fail(rc, "all-reduce of the gradient (stage %d, step %d): %s", stage, step, rmh_last_error());
         // the penalty share of the loss costs a summation launch: only on the steps that report it

@@ -3613,6 +3613,12 @@ struct rm_context {
   std::vector<rm::CamBasis> cams_shadow;    // what the device table holds (the last upload)
   float* batch = nullptr;                   // rm_train_iteration's unfused path: the drawn batch (9 floats/ray)
   float* opt_pre = nullptr;                 // rm_train_iteration: the optimizer part of the launch's extra block
+  // rm_train_step_sampled_prepared: opt_pre holds the next rm_optimizer_step's gradient-independent
+  // part for these arguments (consumed by that call, cleared by any other use of opt_pre)
+  bool opt_prepared = false;
+  const float* prep_raw = nullptr;
+  float* prep_loss_penalty = nullptr;
+  int prep_M = 0, prep_step = 0, prep_pen = 0;
   unsigned* opt_arrival = nullptr;          // rm_train_step_camera_adam: the reduction's column-block counter
   bool adam_done = false;                   // the last call's optimizer ran inside its reduction
   size_t batch_bytes = 0;
@@ -4042,6 +4048,7 @@ int run_small(rm_context* ctx, const Call& c, KArgs& a, long long n) {
     if (extra) {  // the extra block's optimizer part (rm_small.h)
       if (!ctx->opt_pre) RM_HIP(ctx, hipMalloc(&ctx->opt_pre, sizeof(float) * (4 * kOptPreStride + 2)));
       sa.opt_pre = ctx->opt_pre;
+      ctx->opt_prepared = false;  // a preparing call records its arguments after the launch
     }
     hipEvent_t ev0, ev1;
     if ((rc = next_events(ctx, ev0, ev1)) != RM_OK) return rc;
@@ -4904,6 +4911,17 @@ int rm_optimizer_step_f16(rm_context* ctx, float* raw_packed, const float* grad_
   const int M = num_spheres;
   const int n = 7 * M + 4;
   const int nb = (n + 255) / 256;
+  const bool prepared = ctx->opt_prepared && ctx->prep_raw == raw_packed && ctx->prep_M == M &&
+                        ctx->prep_step == step && ctx->prep_pen == (with_penalties ? 1 : 0) &&
+                        ctx->prep_loss_penalty == loss_penalty && !ctx->sdev;
+  ctx->opt_prepared = false;
+  if (prepared) {  // the gradient-independent part ran in the sampled launch (rm_train_step_sampled_prepared)
+    hipLaunchKernelGGL(rm::rm_optimizer_post_small, dim3(1), dim3(256), 0, ctx->stream, raw_packed, grad_act_packed,
+                       adam_m, adam_v, M, lr, weight_decay, act_out, reinterpret_cast<_Float16*>(colors_f16_out),
+                       static_cast<const float*>(ctx->opt_pre));
+    RM_HIP(ctx, hipGetLastError());
+    return RM_OK;
+  }
   if (M <= rm::kOptSmallMaxM && !env_is("RM_OPT_SMALL", '0')) {  // one block: snapshot, repulsion rows, update
     hipLaunchKernelGGL(rm::rm_optimizer_small, dim3(1), dim3(256), 0, ctx->stream, raw_packed, grad_act_packed, adam_m,
                        adam_v, M, step, lr, weight_decay, with_penalties ? 1 : 0, loss_penalty, act_out,
@@ -5047,12 +5065,17 @@ bool sampled_one_launch(const Call& c, int M, long long n) {
 
 extern "C" {
 
-int rm_train_step_sampled(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
-                          int64_t num_src, const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform,
-                          int64_t n_fg, uint64_t seed, uint64_t stream, uint64_t counter, float progress,
-                          float inv_count, const rm_scene* scene, const rm_march* march, const rm_grads* grads,
-                          float* loss_sum) {
+}  // extern "C"
+
+namespace {
+// rm_train_step_sampled[_prepared]; raw_packed != nullptr: prepare the next optimizer step
+int sampled_step(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets, int64_t num_src,
+                 const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform, int64_t n_fg, uint64_t seed,
+                 uint64_t stream, uint64_t counter, float progress, float inv_count, const rm_scene* scene,
+                 const rm_march* march, const rm_grads* grads, float* loss_sum, const float* raw_packed, int32_t step,
+                 int32_t with_penalties, float* loss_penalty) {
   if (!ctx) return RM_ERR_INVALID_ARG;
+  ctx->opt_prepared = false;  // a preparation is for the optimizer call right after its own step
   int rc;
   if ((rc = check_sampling(ctx, ray_org, ray_dir, targets, num_src, fg_indices, num_fg, n_uniform, n_fg)) != RM_OK)
     return rc;
@@ -5085,12 +5108,58 @@ int rm_train_step_sampled(rm_context* ctx, const float* ray_org, const float* ra
     fz.num_fg = num_fg;
     fz.n_uniform = n_uniform;
     fz.key = sample_key(seed, stream, counter);
-    fz.adam = 0;
+    const int M = scene->num_spheres;
+    const bool prep = raw_packed != nullptr && M <= kOptSmallMaxM && !env_is("RM_OPT_SMALL", '0') &&
+                      !env_is("RM_OPT_PREPARE", '0');
+    fz.adam = prep ? 2 : 0;
+    if (prep) {  // the extra block: opt_small_pre of rm_optimizer_small on these parameters
+      fz.raw = const_cast<float*>(raw_packed);
+      fz.m1 = fz.m2 = const_cast<float*>(raw_packed);  // loaded with the parameters, not used
+      fz.step = step;
+      fz.with_pen = with_penalties ? 1 : 0;
+      fz.loss_penalty = loss_penalty;
+    }
     c.fused = &fz;
-    return run(ctx, c);
+    rc = run(ctx, c);
+    if (rc == RM_OK && prep) {
+      ctx->opt_prepared = true;
+      ctx->prep_raw = raw_packed;
+      ctx->prep_loss_penalty = loss_penalty;
+      ctx->prep_M = M;
+      ctx->prep_step = step;
+      ctx->prep_pen = with_penalties ? 1 : 0;
+    }
+    return rc;
   }
   return sample_then_train(ctx, ray_org, ray_dir, targets, num_src, fg_indices, num_fg, n_uniform, n_fg, seed, stream,
                            counter, progress, inv_count, scene, march, grads, loss_sum);
+}
+}  // namespace
+
+extern "C" {
+
+int rm_train_step_sampled(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
+                          int64_t num_src, const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform,
+                          int64_t n_fg, uint64_t seed, uint64_t stream, uint64_t counter, float progress,
+                          float inv_count, const rm_scene* scene, const rm_march* march, const rm_grads* grads,
+                          float* loss_sum) {
+  return sampled_step(ctx, ray_org, ray_dir, targets, num_src, fg_indices, num_fg, n_uniform, n_fg, seed, stream,
+                      counter, progress, inv_count, scene, march, grads, loss_sum, nullptr, 0, 0, nullptr);
+}
+
+int rm_train_step_sampled_prepared(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
+                                   int64_t num_src, const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform,
+                                   int64_t n_fg, uint64_t seed, uint64_t stream, uint64_t counter, float progress,
+                                   float inv_count, const rm_scene* scene, const rm_march* march,
+                                   const rm_grads* grads, float* loss_sum, const float* raw_packed, int32_t step,
+                                   int32_t with_penalties, float* loss_penalty) {
+  if (!ctx) return RM_ERR_INVALID_ARG;
+  if (!raw_packed) return fail(ctx, RM_ERR_INVALID_ARG, "NULL raw parameters");
+  if (step < 1) return fail(ctx, RM_ERR_INVALID_ARG, "step counts from 1");
+  if (ctx->sdev) return fail(ctx, RM_ERR_INVALID_ARG, "prepared steps do not take bound step scalars");
+  return sampled_step(ctx, ray_org, ray_dir, targets, num_src, fg_indices, num_fg, n_uniform, n_fg, seed, stream,
+                      counter, progress, inv_count, scene, march, grads, loss_sum, raw_packed, step, with_penalties,
+                      loss_penalty);
 }
 
 int rm_train_iteration(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,

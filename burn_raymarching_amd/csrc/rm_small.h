@@ -58,7 +58,9 @@ struct SmallArgs {
   float* opt_pre;         // FUSED: [4][kOptPreStride] chain-rule factor and penalty terms per element,
                           // then Adam's two bias corrections (the extra block -> the final block)
   int adam;               // FUSED: 1 -- the extra block and the optimizer step (rm_train_iteration);
-                          // 0 -- the drawn batch's gradient only, for an all-reduce (rm_train_step_sampled)
+                          // 0 -- the drawn batch's gradient only, for an all-reduce (rm_train_step_sampled);
+                          // 2 -- that, and the extra block's optimizer part left in opt_pre for the
+                          // update after the all-reduce (rm_train_step_sampled_prepared)
 };
 constexpr int kOptPreStride = 256;  // >= 7 kSmallMaxM + 4 elements
 static_assert(7 * kSmallMaxM + 4 <= kOptPreStride, "one opt_pre column per element");
@@ -165,7 +167,7 @@ __device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa,
   // FUSED: the optimizer's parameters and moments load while the block sums the records
   OptPrefetch pf;
   if constexpr (FUSED) {
-    if (sa.adam) pf = opt_prefetch(sa.raw, sa.m1, sa.m2, M);
+    if (sa.adam == 1) pf = opt_prefetch(sa.raw, sa.m1, sa.m2, M);
   }
   // The records are read with write-through-cache (sc1) loads only, stored sc1 by every block,
   // each storing wave drained (vmcnt(0)) before the barrier behind which one lane adds to the one
@@ -181,7 +183,7 @@ __device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa,
   RM_TRACE(11, __builtin_amdgcn_s_memrealtime());
   // FUSED: the extra block's optimizer part, loaded with the records (the same hand-off)
   [[maybe_unused]] OptPre opre;
-  if (FUSED && sa.adam) {
+  if (FUSED && sa.adam == 1) {
     const int n = 7 * M + 4;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -275,7 +277,7 @@ __device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa,
   }
   RM_TRACE(9, __builtin_amdgcn_s_memrealtime());
   RM_TRACE(1, __builtin_amdgcn_s_memrealtime());
-  if (FUSED && sa.adam) {
+  if (FUSED && sa.adam == 1) {
     // the optimizer step (rm_optimizer_step: penalties + Adam, train.rs:198) on the gradient just
     // summed (its LDS copy in the packed layout). Every other block has arrived, so nothing reads
     // the activated or raw parameters any more when act_out and raw are overwritten.
@@ -666,4 +668,31 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
   RM_TRACE(1, __builtin_amdgcn_s_memrealtime());
   if (!last) return;
   small_final<FUSED>(a, sa, FUSED && sa.adam ? (int)gridDim.x - 1 : (int)gridDim.x, s_red, ldn, ldlen);
+}
+
+// The update after an all-reduce when the sampled launch's extra block prepared it
+// (rm_train_step_sampled_prepared -> rm_optimizer_step): rm_optimizer_small's opt_small_post on the
+// gradient-independent part read from opt_pre -- the values rm_optimizer_small would compute, so
+// the same bits.
+__global__ __launch_bounds__(256) void rm_optimizer_post_small(float* __restrict__ raw, const float* __restrict__ gact,
+                                                               float* __restrict__ m1, float* __restrict__ m2, int M,
+                                                               float lr, float wd, float* __restrict__ act_out,
+                                                               _Float16* __restrict__ col_h_out,
+                                                               const float* __restrict__ opt_pre) {
+  const OptPrefetch pf = opt_prefetch(raw, m1, m2, M);
+  const int n = 7 * M + 4, tid = (int)threadIdx.x;
+  OptPre o;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int i = tid + 256 * h;
+    float v[4] = {1.0f, 0.0f, 0.0f, 0.0f};
+    if (i < n)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = opt_pre[k * kOptPreStride + i];
+    o.e[h] = ElemPre{v[0], v[1], v[2], v[3], 0.0f};
+  }
+  o.bias.c1 = opt_pre[4 * kOptPreStride];
+  o.bias.c2 = opt_pre[4 * kOptPreStride + 1];
+  const float g[2] = {tid < n ? gact[tid] : 0.0f, tid + 256 < n ? gact[tid + 256] : 0.0f};
+  opt_small_post(o, pf, g, raw, m1, m2, M, lr, wd, act_out, col_h_out);
 }

@@ -90,6 +90,10 @@ SIGNATURES = {
     "rm_train_step_sampled": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _I64, _I64, ctypes.c_uint64,
                                              ctypes.c_uint64, ctypes.c_uint64, _F, _F, ctypes.POINTER(RmScene),
                                              ctypes.POINTER(RmMarch), ctypes.POINTER(RmGrads), _P]),
+    "rm_train_step_sampled_prepared": (ctypes.c_int, [_P, _P, _P, _P, _I64, _P, _I64, _I64, _I64, ctypes.c_uint64,
+                                                      ctypes.c_uint64, ctypes.c_uint64, _F, _F, ctypes.POINTER(RmScene),
+                                                      ctypes.POINTER(RmMarch), ctypes.POINTER(RmGrads), _P, _P, _I32,
+                                                      _I32, _P]),
     "rm_debug_intermediates": (ctypes.c_int, [_P, _P, _P, _I64, ctypes.POINTER(RmScene),
                                               ctypes.POINTER(RmMarch), _P]),
     "rm_debug_order_counts": (ctypes.c_int, [_P, ctypes.POINTER(_I32), _I32, ctypes.POINTER(_I32),

@@ -393,6 +393,22 @@ int rm_train_step_sampled(rm_context* ctx, const float* ray_org, const float* ra
                           float inv_count, const rm_scene* scene, const rm_march* march, const rm_grads* grads,
                           float* loss_sum);
 
+/* rm_train_step_sampled, and in the same launch the gradient-independent part of the optimizer
+ * step that follows the all-reduce (penalties incl. the repulsion rows, the chain-rule factors,
+ * Adam's bias corrections; loss_penalty (nullable) written here) on raw_packed / step /
+ * with_penalties: the next rm_optimizer_step on this context with the same raw_packed,
+ * num_spheres, step, with_penalties and loss_penalty then runs the update only -- the same bits
+ * as without the preparation. Any other call in between that uses the context's optimizer
+ * hand-off, or different arguments, and the optimizer step computes everything itself. Models of
+ * up to 32 spheres and batches of up to 16,384 rays (the one-launch case); otherwise it is
+ * rm_train_step_sampled. Not with bound step scalars (rm_bind_step_scalars). */
+int rm_train_step_sampled_prepared(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
+                                   int64_t num_src, const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform,
+                                   int64_t n_fg, uint64_t seed, uint64_t stream, uint64_t counter, float progress,
+                                   float inv_count, const rm_scene* scene, const rm_march* march,
+                                   const rm_grads* grads, float* loss_sum, const float* raw_packed, int32_t step,
+                                   int32_t with_penalties, float* loss_penalty);
+
 int rm_train_iteration(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,
                        int64_t num_src, const int32_t* fg_indices, int64_t num_fg, int64_t n_uniform, int64_t n_fg,
                        uint64_t seed, uint64_t stream, uint64_t counter, float progress, float inv_count,

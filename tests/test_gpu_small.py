@@ -255,7 +255,21 @@ def _iteration(torch, native, render, model, src, fg, nu, nf, sc, steps, fused, 
         k = 5.0 + 27.0 * it / steps
         march = native.march_params(40, k)
         args = (o.shape[0], p(fg), fg.numel(), nu, nf, 11, 1, it, it / steps, 1.0 / (3 * n))
-        if fused == "sampled":
+        if fused in ("prepared", "prepared_other_step"):
+            # the optimizer's gradient-independent part in the sampled launch; "prepared_other_step"
+            # prepares for another step number, so the optimizer call must compute it itself
+            s = native.RmScene()
+            ctx._lib.rm_scene_from_packed(p(act), m, ctypes.byref(s))
+            g = native.RmGrads()
+            ctx._lib.rm_grads_from_packed(p(grad), m, ctypes.byref(g))
+            prep_step = it if fused == "prepared" else it + 1
+            ctx.check(ctx._lib.rm_train_step_sampled_prepared(ctx.handle, p(o), p(d), p(t), *args, ctypes.byref(s),
+                                                              ctypes.byref(march), ctypes.byref(g), p(loss), p(raw),
+                                                              prep_step, 1, ctypes.c_void_p(loss.data_ptr() + 4)),
+                      "rm_train_step_sampled_prepared")
+            ctx.check(ctx._lib.rm_optimizer_step(ctx.handle, p(raw), p(grad), p(mom[0]), p(mom[1]), m, it, 0.01, 1e-5, 1,
+                                                 ctypes.c_void_p(loss.data_ptr() + 4), p(act)), "rm_optimizer_step")
+        elif fused == "sampled":
             s = native.RmScene()
             ctx._lib.rm_scene_from_packed(p(act), m, ctypes.byref(s))
             g = native.RmGrads()
@@ -426,3 +440,31 @@ def test_train_step_sampled_color_f16(rm, oracle, m):
         out.append((grad.clone(), loss.clone()))
     assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
     assert torch.isfinite(out[0][0]).all() and out[0][1].item() > 0
+
+
+@pytest.mark.parametrize("m,nu,nf,mode", [(7, 13107, 3277, "prepared"), (32, 9000, 7384, "prepared"),
+                                          (9, 13107, 3277, "prepared_other_step"), (40, 13107, 3277, "prepared"),
+                                          (9, 40000, 0, "prepared")])
+def test_train_step_sampled_prepared(rm, oracle, monkeypatch, m, nu, nf, mode):
+    """rm_train_step_sampled_prepared -> rm_optimizer_step (the data-parallel step: the optimizer's
+    gradient-independent part in the sampled launch's extra block, the update alone after the
+    all-reduce) = rm_sample_batch -> rm_train_step -> rm_optimizer_step, bit for bit, with the
+    penalty loss; a preparation for another step number, more than 32 spheres and more than
+    16,384 rays fall back to the full optimizer step, with the same bits."""
+    import torch
+    render, model, native = rm
+    cams = model.ring_cameras(4)
+    rays = [oracle.camera_rays(64, 64, *c, precision="f32") for c in cams]
+    o = np.concatenate([r[0] for r in rays])
+    d = np.concatenate([r[1] for r in rays])
+    tg = oracle.render_diff(o.astype(np.float64), d.astype(np.float64), train_scene(model, 6, 2), 24, 32.0)
+    src = [dev(o), dev(d), dev(tg)]
+    fg = torch.from_numpy(np.flatnonzero(tg.sum(1) > 0.01).astype(np.int32)).cuda()
+    sc = train_scene(model, m, 80 + m)
+    a = _iteration(torch, native, render, model, src, fg, nu, nf, sc, 5, mode, monkeypatch)
+    b = _iteration(torch, native, render, model, src, fg, nu, nf, sc, 5, False, monkeypatch)
+    names = ("raw", "act", "grad", "adam_m", "adam_v", "loss")
+    for it, (xa, xb) in enumerate(zip(a, b)):
+        for name, u, v in zip(names, xa, xb):
+            assert torch.equal(u, v), (it, name, (u - v).abs().max().item())
+    assert a[-1][5][1] > 0  # the penalty share was written
