@@ -12,8 +12,8 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 tail -2 $O/tests.log
 cp $L/libraymarch_hip.so $O/new.so
 for r in 1 2 3; do
-  for v in new finhead; do
-    if [ $v = new ]; then cp $O/new.so $L/libraymarch_hip.so; else cp $L/var/finhead.so $L/libraymarch_hip.so; fi
+  for v in new ${VAR:-finhead}; do
+    if [ $v = new ]; then cp $O/new.so $L/libraymarch_hip.so; else cp $L/var/${VAR:-finhead}.so $L/libraymarch_hip.so; fi
     for mode in single ranks1; do
       extra=""; [ $mode = ranks1 ] && extra="--ranks 1"
       timeout -k 10 120 $L/rm_train train $extra --cameras tests/golden/cameras.json --out $O/train_out --no-previews \
