@@ -122,7 +122,7 @@ def parse():
     ap.add_argument("--scene-json", default=None,
                     help="start from this scene.json (train.rs:238-262 layout, radius + 0.01 re-added as scene.rs:43) "
                          "instead of the synthetic seed-0 scene; --spheres is taken from the file (e.g. a model grown "
-                         "by `rm_train train --split-scale 0 --split-move 0`, BASELINE configs[4])")
+                         "by `rm_train train --split-all --max-spheres 4096`, BASELINE configs[4])")
     ap.add_argument("--fused-adam", choices=["on", "off"], default="off",
                     help="on (one GPU, one call per step): the train step and the optimizer as ONE call "
                          "(rm_train_step_camera_adam: for <= 64 spheres the optimizer runs in the gradient "

@@ -55,13 +55,25 @@ def source_hash(paths=None) -> str:
     return h.hexdigest()[:16]
 
 
-def lib_source_hash(path: str = LIB):
-    """The source hash compiled into a built kernel library (read from the file, not loaded)."""
+def lib_source_hash(path: str = LIB, tag: bytes = rb"\(gfx950\) src "):
+    """The source hash compiled into a built artefact (read from the file, not loaded): the kernel
+    library's rm_version() string by default; HOST_TAG / EXE_TAG for librm_host.so / rm_train."""
     if not os.path.exists(path):
         return None
     with open(path, "rb") as f:
-        m = re.search(rb"\(gfx950\) src ([0-9a-f]{16})", f.read())
+        m = re.search(tag + rb"([0-9a-f]{16})", f.read())
     return m.group(1).decode() if m else None
+
+
+HOST_DIR = os.path.join(CSRC, "host")
+EXE = os.path.join(LIBDIR, "rm_train")
+# librm_host.so's sources (rmh_version(): "host 0.1.0 src <hash>") and rm_train's ("rm_train src
+# <hash>"): each artefact carries the hash of what it was built from, as the kernel library does
+HOST_SOURCES = [os.path.join(HOST_DIR, f) for f in ("io.cpp", "data.cpp", "driver.cpp", "comm.cpp", "rmh_common.hpp")] + \
+    [os.path.join(ROOT, "include", "rm_host.h"), os.path.join(ROOT, "include", "raymarch.h")]
+EXE_SOURCES = [os.path.join(HOST_DIR, "main.cpp"), os.path.join(ROOT, "include", "rm_host.h")]
+HOST_TAG = rb"host 0\.1\.0 src "
+EXE_TAG = rb"rm_train src "
 
 
 def build_lib(force: bool = False, verbose: bool = False) -> str:
@@ -82,31 +94,33 @@ def build_lib(force: bool = False, verbose: bool = False) -> str:
 def build_host(force: bool = False, verbose: bool = False) -> str:
     """librm_host.so (include/rm_host.h: files, dataset, prune_and_split, train driver) and the
     rm_train CLI, both C++ host code linked against libraymarch_hip.so."""
-    host_dir = os.path.join(CSRC, "host")
+    host_dir = HOST_DIR
     if not os.path.isdir(host_dir):
         return ""
     lib = build_lib(force=force, verbose=verbose)
     inc = os.path.join(ROOT, "include")
-    headers = [os.path.join(inc, "raymarch.h"), os.path.join(inc, "rm_host.h"),
-               os.path.join(host_dir, "rmh_common.hpp")]
-    lib_srcs = [os.path.join(host_dir, f) for f in ("io.cpp", "data.cpp", "driver.cpp", "comm.cpp")]
+    lib_srcs = [p for p in HOST_SOURCES if p.endswith(".cpp")]
     # -ffp-contract=off: the host f32 arithmetic (camera rays, prune_and_split) keeps the
     # reference's rounding, no fused multiply-adds
     common = [_hipcc(), "-O2", "-std=c++17", "-Wall", "-fPIC", "-ffp-contract=off", "-I", inc]
     rpath = ["-Wl,-rpath,$ORIGIN"]
-    if force or _stale(HOST_LIB, lib_srcs + headers + [lib]):
-        cmd = common + ["-shared", "-o", HOST_LIB] + lib_srcs + ["-L", LIBDIR, "-lraymarch_hip", "-lz", "-lrccl"] + rpath
+    # rebuilt when the embedded hash differs from the tree's (not on mtimes alone), or when a
+    # source or the library it links is newer
+    hsha = source_hash(HOST_SOURCES)
+    if force or _stale(HOST_LIB, HOST_SOURCES + [lib]) or lib_source_hash(HOST_LIB, HOST_TAG) != hsha:
+        cmd = common + [f'-DRMH_SOURCE_SHA="{hsha}"', "-shared", "-o", HOST_LIB] + lib_srcs + \
+            ["-L", LIBDIR, "-lraymarch_hip", "-lz", "-lrccl"] + rpath
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
-    exe = os.path.join(LIBDIR, "rm_train")
-    main = os.path.join(host_dir, "main.cpp")
-    if force or _stale(exe, [main, HOST_LIB] + headers):
-        cmd = common + ["-o", exe, main, "-L", LIBDIR, "-lrm_host", "-lraymarch_hip"] + rpath
+    esha = source_hash(EXE_SOURCES)
+    if force or _stale(EXE, EXE_SOURCES + [HOST_LIB]) or lib_source_hash(EXE, EXE_TAG) != esha:
+        cmd = common + [f'-DRMT_SOURCE_SHA="{esha}"', "-o", EXE, EXE_SOURCES[0], "-L", LIBDIR, "-lrm_host",
+                        "-lraymarch_hip"] + rpath
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
-    return exe
+    return EXE
 
 
 def build_all(force: bool = False, verbose: bool = False) -> None:

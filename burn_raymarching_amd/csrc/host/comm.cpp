@@ -91,9 +91,18 @@ int rccl_wait(void* state, void* stream) {
     const double waited = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
     if (s && waited > s->timeout_s) {
       rccl_abort(s);  // ends this rank's pending collectives so the stream drains
-      (void)hipStreamSynchronize((hipStream_t)stream);
+      // the abort ends RCCL's kernels, not others': give the stream a bounded grace to drain and
+      // return the error either way (an unbounded hipStreamSynchronize would hang the watchdog
+      // itself behind a stuck non-collective kernel)
+      const double grace = s->timeout_s < 10.0 ? s->timeout_s : 10.0;
+      const auto ta = std::chrono::steady_clock::now();
+      bool drained = false;
+      while (!(drained = hipStreamQuery((hipStream_t)stream) != hipErrorNotReady) &&
+             std::chrono::duration<double>(std::chrono::steady_clock::now() - ta).count() < grace)
+        std::this_thread::sleep_for(std::chrono::milliseconds(1));
       return fail(RMH_ERR_GPU, "the stream did not drain within %.1f s (a peer rank left a collective?); "
-                  "communicator aborted", s->timeout_s);
+                  "communicator aborted, stream %s", s->timeout_s,
+                  drained ? "drained after the abort" : "still busy after the abort's grace period");
     }
     // spin briefly (the common case: a few microseconds of work left), then back off
     if (polls < 200) std::this_thread::yield();

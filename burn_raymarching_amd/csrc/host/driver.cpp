@@ -401,8 +401,15 @@ int rmh_train(const rmh_train_config* cfg, rmh_train_result* result, float* raw_
         if ((rc = sync_stream(g, comm)) != RMH_OK) return rc;
         const float* s = h_loss.f();
         last_loss = s[0] * inv_count + s[1];  // training.rs:34 + penalties
-        if (verbose && step % cfg->log_every == 0)
-          std::printf("  Step %d | Loss: %.5f | k: %.1f\n", step, last_loss, march.smooth_k);
+        if (verbose && step % cfg->log_every == 0) {
+          std::printf("  Step %d | Loss: %.5f | k: %.1f", step, last_loss, march.smooth_k);
+          if (const char* e = std::getenv("RMH_LOG_BITS"); e && e[0] == '1') {  // diagnosis: the loss bits
+            uint32_t b[2];
+            std::memcpy(b, s, sizeof b);
+            std::printf(" | bits %08x %08x", b[0], b[1]);
+          }
+          std::printf("\n");
+        }
       }
     }
     const auto t_enq = std::chrono::steady_clock::now();  // the host has issued the stage's steps

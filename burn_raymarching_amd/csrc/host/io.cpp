@@ -376,6 +376,11 @@ extern "C" {
 
 const char* rmh_last_error(void) { return g_err.c_str(); }
 
+#ifndef RMH_SOURCE_SHA
+#define RMH_SOURCE_SHA "unknown"  // _build.py passes the sha256 of the host sources
+#endif
+const char* rmh_version(void) { return "burn_raymarching_amd host 0.1.0 src " RMH_SOURCE_SHA; }
+
 void rmh_free(void* p) { std::free(p); }
 
 int rmh_png_read(const char* path, int32_t* width, int32_t* height, uint8_t** rgb) {

@@ -11,7 +11,8 @@
 //     for them. (--rank r --world N --comm-file F [--run-id S] [--comm-timeout SEC] run one rank
 //     of a run launched elsewhere: every rank of the run gets the same F and S.)
 //     --split-scale / --split-move: prune_and_split's split threshold scale and minimum move
-//     (rmh_train_config: 0 = the reference's 1 / 0.05, negative = no such condition);
+//     (negative = no such condition; an explicit 0 is refused: rmh_train_config reads 0 as the
+//     reference's 1 / 0.05, where rmh_prune_and_split_ex's 0 / 0 splits every sphere);
 //     --split-all: every surviving sphere splits (both negative: growth runs such as BASELINE
 //     configs[4]); --max-spheres caps the next generation, 0 = no cap;
 //     --color-f16: fp16 colour / fp32 SDF.
@@ -67,9 +68,15 @@ int train_rank(rmh_train_config cfg, int rank, int world, const char* comm_file,
   const int rc = rmh_train(&cfg, &res, nullptr, 0);
   if (cfg.comm) rmh_collective_rccl_destroy(&comm);
   if (rc == RMH_OK && rank <= 0)
-    std::printf("{\"num_spheres\": %d, \"steps\": %d, \"final_loss\": %.6g, \"seconds\": %.4f, \"step_ms\": %.4f, "
-                "\"ranks\": %d}\n",
-                res.num_spheres, res.steps, res.final_loss, res.seconds, res.step_ms, world);
+  {
+    // final_loss_bits: the loss's fp32 bit pattern, so that a run can be compared bit for bit
+    uint32_t bits = 0;
+    const float fl = (float)res.final_loss;
+    std::memcpy(&bits, &fl, sizeof bits);
+    std::printf("{\"num_spheres\": %d, \"steps\": %d, \"final_loss\": %.6g, \"final_loss_bits\": \"%08x\", "
+                "\"seconds\": %.4f, \"step_ms\": %.4f, \"ranks\": %d}\n",
+                res.num_spheres, res.steps, res.final_loss, bits, res.seconds, res.step_ms, world);
+  }
   return report(rc, "train");
 }
 
@@ -123,9 +130,17 @@ int launch_ranks(const rmh_train_config& cfg, int n, double comm_timeout) {
 
 }  // namespace
 
+#ifndef RMT_SOURCE_SHA
+#define RMT_SOURCE_SHA "unknown"  // _build.py passes the sha256 of main.cpp and rm_host.h
+#endif
+
 int main(int argc, char** argv) {
   if (argc < 2) return usage();
   const std::string cmd = argv[1];
+  if (cmd == "--version") {  // this program's sources, then the host library's (see rmh_version)
+    std::printf("rm_train src " RMT_SOURCE_SHA "\n%s\n", rmh_version());
+    return 0;
+  }
   auto need = [&](int i) { return i + 1 < argc; };
   if (cmd == "train") {
     rmh_train_config cfg;
@@ -179,10 +194,17 @@ int main(int argc, char** argv) {
         run_id = argv[++i];
       } else if (a == "--comm-timeout") {
         comm_timeout = std::atof(argv[++i]);
-      } else if (a == "--split-scale") {
-        cfg.split_scale = (float)std::atof(argv[++i]);
-      } else if (a == "--split-move") {
-        cfg.split_move = (float)std::atof(argv[++i]);
+      } else if (a == "--split-scale" || a == "--split-move") {
+        // 0 in rmh_train_config means "the reference value" (1 / 0.05), where prune_and_split_ex's
+        // 0 / 0 splits every sphere: an explicit 0 here is refused so that an old "split everything"
+        // command line cannot silently run the reference rule (use --split-all)
+        const float v = (float)std::atof(argv[++i]);
+        if (v == 0.0f) {
+          std::fprintf(stderr, "%s 0 is ambiguous: use --split-all to split every sphere, or omit it for the "
+                       "reference value\n", a.c_str());
+          return 2;
+        }
+        (a == "--split-scale" ? cfg.split_scale : cfg.split_move) = v;
       } else if (a == "--max-spheres") {
         cfg.max_spheres = std::atoi(argv[++i]);
       } else {

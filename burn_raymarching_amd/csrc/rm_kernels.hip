@@ -693,6 +693,28 @@ __device__ __forceinline__ f2 qpair(const f2& PX, const f2& PY, const f2& PZ, co
 }
 __device__ __forceinline__ float psq(const float p[3]) { return fmaf(p[2], p[2], fmaf(p[1], p[1], p[0] * p[0])); }
 
+// The light direction ld / |ld| (renderer_diff.rs:49-50) and the Jacobian of that normalisation
+// applied to summed per-ray terms r: component k of (r - ldn (ldn . r)) / |ld|. Contraction off in
+// both: every kernel (general and small, forward and final blocks) forms them with the same fp32
+// operations whatever code surrounds the call, so their bits cannot follow unrelated edits.
+__device__ __forceinline__ float light_unit(const float* light_dir, float (&ln)[3]) {
+#pragma clang fp contract(off)
+  const float l0 = light_dir[0], l1 = light_dir[1], l2 = light_dir[2];
+  const float len = sqrtf(l0 * l0 + l1 * l1 + l2 * l2);
+  ln[0] = l0 / len;
+  ln[1] = l1 / len;
+  ln[2] = l2 / len;
+  return len;
+}
+__device__ __forceinline__ float light_grad(const float (&r)[3], const float* light_dir, int k) {
+#pragma clang fp contract(off)
+  float ln[3];
+  const float len = light_unit(light_dir, ln);
+  const float proj = ln[0] * r[0] + ln[1] * r[1] + ln[2] * r[2];
+  const float rk = k == 0 ? r[0] : (k == 1 ? r[1] : r[2]), lk = k == 0 ? ln[0] : (k == 1 ? ln[1] : ln[2]);
+  return (rk - lk * proj) / len;
+}
+
 // A wave's 64 spheres' 8 record columns (lane = sphere, v[7] = 0) stored as two contiguous 1 KB
 // runs: store h covers spheres 32 h .. 32 h + 31, lane l writing half (l & 1) of sphere
 // 32 h + (l >> 1) (two half-line stores per lane would touch every line twice). Every lane of
@@ -2218,12 +2240,8 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       ldn[1] = a.light_fixed[1];
       ldn[2] = a.light_fixed[2];
     } else {
-      const float ld0 = a.light_dir[0], ld1 = a.light_dir[1], ld2 = a.light_dir[2];
       amb = a.ambient[0];
-      const float ldlen = sqrtf(ld0 * ld0 + ld1 * ld1 + ld2 * ld2);
-      ldn[0] = ld0 / ldlen;
-      ldn[1] = ld1 / ldlen;
-      ldn[2] = ld2 / ldlen;
+      light_unit(a.light_dir, ldn);
     }
     sdot = fmaf(nrm[2], ldn[2], fmaf(nrm[1], ldn[1], nrm[0] * ldn[0]));
     dif = fmaxf(sdot, 0.0f);
@@ -3049,17 +3067,8 @@ __global__ __launch_bounds__(256) void rm_reduce_partials(const float* __restric
 // Pass 2 for the 256 columns of pass-1 column block blockIdx.x, by the block of that column block
 // that arrived last: thread t sums column t's kReduceSegs segments in the four chains s mod 4 of
 // rm_finalize_grads, combined (a0 + a1) + (a2 + a3) -- the same bits -- then the scatter.
-// The light-direction gradient (renderer_diff.rs:49-50, the Jacobian of ld / |ld|) of the summed
-// per-ray terms r: component k of (r - ldn (ldn . r)) / |ld|. One function with contraction off for
-// both pass-2 forms (finalize_block, rm_finalize_grads), so that they give the same bits.
-__device__ __forceinline__ float light_grad(const float (&r)[3], const float* light_dir, int k) {
-#pragma clang fp contract(off)
-  const float l0 = light_dir[0], l1 = light_dir[1], l2 = light_dir[2];
-  const float len = sqrtf(l0 * l0 + l1 * l1 + l2 * l2);
-  const float ln[3] = {l0 / len, l1 / len, l2 / len};
-  const float proj = ln[0] * r[0] + ln[1] * r[1] + ln[2] * r[2];
-  return (r[k] - ln[k] * proj) / len;
-}
+// The light-direction gradient: light_grad (contraction off), the same function in both pass-2
+// forms (finalize_block, rm_finalize_grads) and in the small kernel's final block.
 
 // a gradient element of the final scatter: write-through when the fused optimizer reads it
 __device__ __forceinline__ void put_grad(const FinalArgs& f, float* dst, float v) {
@@ -3178,6 +3187,7 @@ __device__ __forceinline__ float softplusf_(float x) { return logf(1.0f + expf(x
 
 // scene.rs:41-45 on packed element i (layout [centers 3M | colors 3M | radius M | light 3 | ambient 1]).
 __device__ __forceinline__ float activate_elem(float x, int i, int M) {
+#pragma clang fp contract(off)
   if (i < 3 * M) return x;                           // centers
   if (i < 6 * M) return sigmoidf_(x);                // colors = sigmoid(raw)        scene.rs:41
   if (i < 7 * M) return softplusf_(x) + 0.01f;       // radius = softplus(raw)+0.01  scene.rs:43
@@ -3264,6 +3274,7 @@ __device__ __forceinline__ void block_sum4(float (&v)[4], float* red) {
 // v[3], its gradient w.r.t. c_s through both the (s, j) and (j, s) entries into v[0..2].
 // c: the pre-step centres [M][3] (raw = activated).
 __device__ __forceinline__ void repulsion_row(const float* c, int M, int s, int j0, int stride, float (&v)[4]) {
+#pragma clang fp contract(off)
   const float cx = c[3 * s], cy = c[3 * s + 1], cz = c[3 * s + 2];
   const float csq = cx * cx + cy * cy + cz * cz;
   for (int j = j0; j < M; j += stride) {
@@ -3305,7 +3316,10 @@ __global__ __launch_bounds__(256) void rm_penalty_pairs(const float* __restrict_
 
 // One parameter element i of the packed layout: chain rule of the activations, the compute_loss
 // penalties (training.rs:38-82), coupled weight decay and Burn's Adam; optionally the activated
-// parameters of the updated model (scene.rs:41-45) for the next step's render. Split in two: the
+// parameters of the updated model (scene.rs:41-45) for the next step's render. Contraction is off
+// in these functions (explicit fmaf where a fused multiply-add is meant): the optimizer runs inside
+// several kernels (its own launches, the reduction's and the small kernel's last blocks), and its
+// bits must not depend on which. Split in two: the
 // part that depends on the pre-step parameters only (optimizer_pre: the chain-rule factor, the
 // penalties' gradient terms and loss share -- the fused iteration runs it while the gradient is
 // still being summed) and the update itself (optimizer_apply).
@@ -3316,6 +3330,7 @@ struct ElemPre {
 };
 // raw: the pre-step parameters (a snapshot: neighbours are read); pair: the repulsion rows.
 __device__ __forceinline__ ElemPre optimizer_pre(int i, const float* raw, const float* pair, int M, int with_pen) {
+#pragma clang fp contract(off)
   ElemPre e{1.0f, 0.0f, 0.0f, 0.0f, 0.0f};
   const float x = raw[i];
   const float invM = 1.0f / (float)M;
@@ -3379,6 +3394,7 @@ __device__ __forceinline__ void optimizer_apply(int i, const ElemPre& e, float g
                                                 float* __restrict__ raw_out, float* __restrict__ m1,
                                                 float* __restrict__ m2, float* __restrict__ act_out,
                                                 _Float16* __restrict__ col_h_out) {
+#pragma clang fp contract(off)
   float gv = ((g * e.fac + e.t0) + e.t1) + e.t2;
   gv = fmaf(wd, x, gv);
   const float b1 = 0.9f, b2 = 0.999f, eps = 1e-5f;
@@ -3586,6 +3602,17 @@ __global__ void rm_sum_small(const float* __restrict__ parts, int n, float* __re
 
 #include "rm_small.h"
 
+// rm_debug_stall: one wave that holds its stream until the host sets *flag (a system-scope load
+// of host-mapped memory, polled with s_sleep) or max_ticks of the 100 MHz real-time counter have
+// passed -- every run of it ends by itself. Tests use it to stand for a stuck collective.
+__global__ __launch_bounds__(64) void rm_stall_kernel(const int* flag, unsigned long long max_ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > max_ticks) break;
+    __builtin_amdgcn_s_sleep(100);
+  }
+}
+
 }  // namespace rm
 
 // =======================================================================================
@@ -3630,6 +3657,7 @@ struct rm_context {
   int* olist = nullptr;                     // cost-ordered dispatch: 3 x [class][kMaxBlocksPerLaunch] block lists
   int* ocnt = nullptr;                      // 3 x [class] list lengths (zeroed one launch ahead)
   float* cont_buf = nullptr;                // split continuation: saved march state | list | count
+  int* stall_flag = nullptr;                // rm_debug_stall: host-mapped release flag (host pointer)
   size_t cont_bytes = 0;
   int* oturn = nullptr;                     // device word: the list set the next keyed launch appends to
   unsigned long long cost_key = 0;          // geometry of the last keyed launch (its lists order the next)
@@ -4145,6 +4173,9 @@ int upload_cams(rm_context* ctx, const Call& c, KArgs& a) {
 
 int run(rm_context* ctx, const Call& c) {
   if (!ctx) return RM_ERR_INVALID_ARG;
+  // a prepared optimizer step is for the rm_optimizer_step right after its own sampled step: any
+  // other call in between may change the parameters it was prepared on (sampled_step sets it again)
+  ctx->opt_prepared = false;
   int rc;
   if ((rc = check_scene(ctx, c.scene, c.mode != kRender)) != RM_OK) return rc;
   if ((rc = check_march(ctx, c.march)) != RM_OK) return rc;
@@ -4542,6 +4573,26 @@ int rm_debug_block_trace(rm_context* ctx, unsigned long long* host, int64_t cap_
 }
 #endif
 
+int rm_debug_stall(rm_context* ctx, int32_t max_ms) {
+  if (!ctx) return RM_ERR_INVALID_ARG;
+  if (max_ms < 1 || max_ms > 600000) return fail(ctx, RM_ERR_INVALID_ARG, "max_ms %d out of [1, 600000]", max_ms);
+  if (!ctx->stall_flag)
+    RM_HIP(ctx, hipHostMalloc(reinterpret_cast<void**>(&ctx->stall_flag), 64, hipHostMallocMapped | hipHostMallocCoherent));
+  __atomic_store_n(ctx->stall_flag, 0, __ATOMIC_RELEASE);
+  int* dflag = nullptr;
+  RM_HIP(ctx, hipHostGetDevicePointer(reinterpret_cast<void**>(&dflag), ctx->stall_flag, 0));
+  hipLaunchKernelGGL(rm::rm_stall_kernel, dim3(1), dim3(64), 0, ctx->stream, dflag,
+                     (unsigned long long)max_ms * 100000ull);  // s_memrealtime: 100 MHz
+  RM_HIP(ctx, hipGetLastError());
+  return RM_OK;
+}
+
+int rm_debug_stall_release(rm_context* ctx) {
+  if (!ctx) return RM_ERR_INVALID_ARG;
+  if (ctx->stall_flag) __atomic_store_n(ctx->stall_flag, 1, __ATOMIC_RELEASE);
+  return RM_OK;
+}
+
 int rm_stats_enable(rm_context* ctx, int32_t enable) {
   if (!ctx) return RM_ERR_INVALID_ARG;
   if (enable && !ctx->stats_dev) {
@@ -4583,6 +4634,11 @@ int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset) {
 
 void rm_destroy(rm_context* ctx) {
   if (!ctx) return;
+  if (ctx->stall_flag) {  // a pending stall ends before its flag goes away
+    __atomic_store_n(ctx->stall_flag, 1, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipHostFree(ctx->stall_flag);
+  }
   if (ctx->stats_dev || ctx->esc_flags || ctx->rec || ctx->block_order || ctx->olist || ctx->cont_buf) {
     (void)hipStreamSynchronize(ctx->stream);
     if (ctx->stats_dev) (void)hipFree(ctx->stats_dev);
@@ -4816,6 +4872,7 @@ int rm_debug_intermediates(rm_context* ctx, const float* ray_org, const float* r
 
 int rm_scene_activate(rm_context* ctx, const float* raw_packed, int32_t num_spheres, float* act_packed) {
   if (!ctx) return RM_ERR_INVALID_ARG;
+  ctx->opt_prepared = false;  // the parameters may have changed since a prepared step (see run)
   if (!raw_packed || !act_packed) return fail(ctx, RM_ERR_INVALID_ARG, "NULL packed buffer");
   if (num_spheres < 1 || num_spheres > RM_MAX_SPHERES) return fail(ctx, RM_ERR_INVALID_ARG, "bad num_spheres");
   const int n = 7 * num_spheres + 4;
@@ -4829,6 +4886,7 @@ int rm_gather_rays(rm_context* ctx, const float* ray_org, const float* ray_dir, 
                    int64_t num_src, const int32_t* indices, int64_t num_rays, float* out_org, float* out_dir,
                    float* out_targets) {
   if (!ctx) return RM_ERR_INVALID_ARG;
+  ctx->opt_prepared = false;
   if (num_rays < 0 || num_src < 0) return fail(ctx, RM_ERR_INVALID_ARG, "negative size");
   if (num_rays == 0) return RM_OK;
   if (!indices) return fail(ctx, RM_ERR_INVALID_ARG, "indices is NULL");
@@ -4865,6 +4923,7 @@ int rm_sample_batch(rm_context* ctx, const float* ray_org, const float* ray_dir,
                     uint64_t stream, uint64_t counter, float* out_org, float* out_dir, float* out_targets,
                     int32_t* indices_out) {
   if (!ctx) return RM_ERR_INVALID_ARG;
+  ctx->opt_prepared = false;
   if (num_src < 0 || num_fg < 0 || n_uniform < 0 || n_fg < 0) return fail(ctx, RM_ERR_INVALID_ARG, "negative size");
   const long long n = n_uniform + n_fg;
   if (n == 0) return RM_OK;
@@ -4968,6 +5027,7 @@ int rm_train_step_camera_adam(rm_context* ctx, const rm_camera* cams, int32_t nu
                               float weight_decay, int32_t with_penalties, float* loss_sum, float* loss_penalty,
                               uint16_t* colors_f16_out) {
   if (!ctx) return RM_ERR_INVALID_ARG;
+  ctx->opt_prepared = false;
   if (!act_packed || !grad_packed || !raw_packed || !adam_m || !adam_v || !march)
     return fail(ctx, RM_ERR_INVALID_ARG, "NULL model buffer");
   if (num_spheres < 1 || num_spheres > RM_MAX_SPHERES) return fail(ctx, RM_ERR_INVALID_ARG, "bad num_spheres");
@@ -5169,6 +5229,7 @@ int rm_train_iteration(rm_context* ctx, const float* ray_org, const float* ray_d
                        float* adam_m, float* adam_v, int32_t num_spheres, int32_t step, float lr,
                        float weight_decay, int32_t with_penalties, float* loss_sum, float* loss_penalty) {
   if (!ctx) return RM_ERR_INVALID_ARG;
+  ctx->opt_prepared = false;
   int rc;
   if ((rc = check_sampling(ctx, ray_org, ray_dir, targets, num_src, fg_indices, num_fg, n_uniform, n_fg)) != RM_OK)
     return rc;

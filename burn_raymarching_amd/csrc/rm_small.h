@@ -29,6 +29,9 @@
 #pragma once
 
 constexpr int kSmallMaxM = 32;             // spheres handled by the small kernel
+#ifndef RM_SMALL_PAR_TOTALS
+#define RM_SMALL_PAR_TOTALS 1  // final block: column totals formed once in parallel (0: per use)
+#endif
 #ifndef RM_SMALL_FIN_BATCH
 #define RM_SMALL_FIN_BATCH 32  // record rows in flight per thread in the final block's sums
 #endif
@@ -153,13 +156,11 @@ __device__ __forceinline__ bool small_arrive(const SmallArgs& sa, int* s_last) {
 }
 
 // The last block: sum the nrows blocks' records and write the gradients (rm_finalize_grads'
-// layout and light-direction Jacobian; ldn / ldlen: ld / |ld| and |ld| of the scene's light_dir,
-// as the shade stage forms them); FUSED: then the optimizer update on that gradient, with the
+// layout and light-direction Jacobian, light_grad: contraction off); FUSED: then the optimizer update on that gradient, with the
 // gradient-independent part the launch's extra block left in sa.opt_pre. s_red: the kernel's
 // cross-wave LDS buffer (free by now).
 template <bool FUSED>
-__device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa, int nrows, float* s_red,
-                                            const float (&ldn)[3], float ldlen) {
+__device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa, int nrows, float* s_red) {
   const int tid = threadIdx.x;
   const int M = a.M, Mpad = a.Mpad;
   const int nneed = M * 8 + 8;  // columns of the real spheres, then the scalars
@@ -236,11 +237,27 @@ __device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa,
   __syncthreads();
   RM_TRACE(2, __builtin_amdgcn_s_memrealtime());
   const FinalArgs& f = sa.fin;
+  // a column's total: its chains added in order. RM_SMALL_PAR_TOTALS: every column's total formed
+  // once, by all threads in parallel, behind one barrier (the same adds in the same order as
+  // forming it in each lane that uses it; s_red holds chains * nneed <= kBlock + 8 floats, the
+  // totals go above them)
+  static_assert(2 * (kBlock + 32) + 8 <= kWaves * (kSmallMaxM * 8 + 8), "s_red holds the chains and the totals");
+#if RM_SMALL_PAR_TOTALS
+  float* s_tot = s_red + kBlock + 32;
+  for (int idx = tid; idx < nneed; idx += kBlock) {
+    float v = s_red[idx];
+    for (int ch = 1; ch < chains; ++ch) v += s_red[ch * nneed + idx];
+    s_tot[idx] = v;
+  }
+  __syncthreads();
+  auto total = [&](int idx) { return s_tot[idx]; };
+#else
   auto total = [&](int idx) {
     float v = s_red[idx];
     for (int ch = 1; ch < chains; ++ch) v += s_red[ch * nneed + idx];
     return v;
   };
+#endif
   // FUSED: the gradient also goes to LDS in the packed layout the optimizer reads
   [[maybe_unused]] float* s_gact = nullptr;
   if constexpr (FUSED) {
@@ -261,10 +278,7 @@ __device__ __forceinline__ void small_final(const KArgs& a, const SmallArgs& sa,
   if (tid < 3) {
     if (f.gld) {
       const float sc[3] = {total(M * 8), total(M * 8 + 1), total(M * 8 + 2)};
-      const float proj = ldn[0] * sc[0] + ldn[1] * sc[1] + ldn[2] * sc[2];
-      const float mine = tid == 0 ? sc[0] : (tid == 1 ? sc[1] : sc[2]);
-      const float ln = tid == 0 ? ldn[0] : (tid == 1 ? ldn[1] : ldn[2]);
-      const float gv = (mine - ln * proj) / ldlen;
+      const float gv = light_grad(sc, a.light_dir, tid);
       store_or_add(f.gld + tid, gv, f.accumulate);
       if constexpr (FUSED) s_gact[7 * M + tid] = gv;
     }
@@ -340,14 +354,10 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
         __hip_atomic_store(sa.opt_pre + 4 * kOptPreStride, o.bias.c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_store(sa.opt_pre + 4 * kOptPreStride + 1, o.bias.c2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      // the final block's light Jacobian, if this block arrives last (the shade stage's expressions)
-      const float ld0 = a.light_dir[0], ld1 = a.light_dir[1], ld2 = a.light_dir[2];
-      const float ldlen = sqrtf(ld0 * ld0 + ld1 * ld1 + ld2 * ld2);
-      const float ldn[3] = {ld0 / ldlen, ld1 / ldlen, ld2 / ldlen};
       const bool last = small_arrive(sa, &s_last);
       RM_TRACE(8, __builtin_amdgcn_s_memrealtime());
       RM_TRACE(1, __builtin_amdgcn_s_memrealtime());
-      if (last) small_final<FUSED>(a, sa, (int)gridDim.x - 1, s_red, ldn, ldlen);
+      if (last) small_final<FUSED>(a, sa, (int)gridDim.x - 1, s_red);
       return;
     }
   }
@@ -527,10 +537,9 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
   const float inv_len = frsq(fmaf(nz, nz, fmaf(ny, ny, fmaf(nx, nx, 1e-6f))));
   const float nrm[3] = {nx * inv_len, ny * inv_len, nz * inv_len};
   // ---- lighting (renderer_diff.rs:48-62)
-  const float ld0 = a.light_dir[0], ld1 = a.light_dir[1], ld2 = a.light_dir[2];
   const float amb = a.ambient[0];
-  const float ldlen = sqrtf(ld0 * ld0 + ld1 * ld1 + ld2 * ld2);
-  const float ldn[3] = {ld0 / ldlen, ld1 / ldlen, ld2 / ldlen};
+  float ldn[3];
+  light_unit(a.light_dir, ldn);
   const float sdot = fmaf(nrm[2], ldn[2], fmaf(nrm[1], ldn[1], nrm[0] * ldn[0]));
   const float dif = fmaxf(sdot, 0.0f);
   const float Lgt = fmaf(dif, 1.0f - amb, amb);
@@ -667,7 +676,7 @@ __global__ __launch_bounds__(kBlock, 1) void rm_small_kernel(const KArgs a, cons
   RM_TRACE(8, __builtin_amdgcn_s_memrealtime());
   RM_TRACE(1, __builtin_amdgcn_s_memrealtime());
   if (!last) return;
-  small_final<FUSED>(a, sa, FUSED && sa.adam ? (int)gridDim.x - 1 : (int)gridDim.x, s_red, ldn, ldlen);
+  small_final<FUSED>(a, sa, FUSED && sa.adam ? (int)gridDim.x - 1 : (int)gridDim.x, s_red);
 }
 
 // The update after an all-reduce when the sampled launch's extra block prepared it

@@ -15,6 +15,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.environ.get("RMH_LIB_PATH", os.path.join(_HERE, "lib", "librm_host.so"))
 
 RMH_OK = 0
+RMH_ERR_GPU = 4
 _ERR_NAMES = {1: "RMH_ERR_INVALID_ARG", 2: "RMH_ERR_IO", 3: "RMH_ERR_FORMAT", 4: "RMH_ERR_GPU"}
 RMH_PATH_MAX = 512
 
@@ -111,6 +112,7 @@ SIGNATURES = {
     "rmh_train": (ctypes.c_int, [ctypes.POINTER(RmhTrainConfig), ctypes.POINTER(RmhTrainResult), _P, _I32]),
     "rmh_preview": (ctypes.c_int, [_S, _S, _I32, _I32, _P, _P, _F, _F, _I32]),
     "rmh_generate": (ctypes.c_int, [_S, _S, _I32, _I32, _I32]),
+    "rmh_version": (ctypes.c_char_p, []),
 }
 
 _lib = None

@@ -98,6 +98,8 @@ SIGNATURES = {
                                               ctypes.POINTER(RmMarch), _P]),
     "rm_debug_order_counts": (ctypes.c_int, [_P, ctypes.POINTER(_I32), _I32, ctypes.POINTER(_I32),
                                              ctypes.POINTER(_I32)]),
+    "rm_debug_stall": (ctypes.c_int, [_P, _I32]),
+    "rm_debug_stall_release": (ctypes.c_int, [_P]),
     "rm_timing_enable": (ctypes.c_int, [_P, _I32]),
     "rm_timing_collect": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_I64), _I32]),
     "rm_stats_enable": (ctypes.c_int, [_P, _I32]),

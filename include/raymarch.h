@@ -280,6 +280,12 @@ int rm_debug_intermediates(rm_context* ctx, const float* ray_org, const float* r
  * uncleared (the state a failed launch in the rotation leaves), for the recovery test. */
 int rm_debug_order_counts(rm_context* ctx, int32_t* counts, int32_t capacity, int32_t* classes, int32_t* next_set);
 
+/* Stream stall (tests of a caller's watchdog, e.g. rmh_collective.wait): enqueues on the context's
+ * stream one wave that spins until rm_debug_stall_release(ctx) or until max_ms (1 .. 600000) have
+ * passed, whichever comes first -- it always ends by itself. rm_destroy releases a pending one. */
+int rm_debug_stall(rm_context* ctx, int32_t max_ms);
+int rm_debug_stall_release(rm_context* ctx);
+
 /* ---- kernel timing (benchmark instrumentation) ------------------------------ */
 /* rm_timing_enable(ctx, 1): every later render / backward / train call records a
  * hipEvent pair around each launch of its main per-ray kernel on the context's
@@ -398,8 +404,12 @@ int rm_train_step_sampled(rm_context* ctx, const float* ray_org, const float* ra
  * Adam's bias corrections; loss_penalty (nullable) written here) on raw_packed / step /
  * with_penalties: the next rm_optimizer_step on this context with the same raw_packed,
  * num_spheres, step, with_penalties and loss_penalty then runs the update only -- the same bits
- * as without the preparation. Any other call in between that uses the context's optimizer
- * hand-off, or different arguments, and the optimizer step computes everything itself. Models of
+ * as without the preparation. The contents of raw_packed (and of the buffers the gradient comes
+ * from) must not change between the two calls except through the caller's all-reduce of the
+ * gradient: the library cannot see a host copy into raw_packed or a parameter broadcast, and the
+ * update would use the factors prepared on the old values. Any other call of this library on the
+ * context in between (every render, train, sampling, gather and activation entry point) drops the
+ * preparation, as do different arguments: the optimizer step then computes everything itself. Models of
  * up to 32 spheres and batches of up to 16,384 rays (the one-launch case); otherwise it is
  * rm_train_step_sampled. Not with bound step scalars (rm_bind_step_scalars). */
 int rm_train_step_sampled_prepared(rm_context* ctx, const float* ray_org, const float* ray_dir, const float* targets,

@@ -38,6 +38,11 @@ extern "C" {
 
 const char* rmh_last_error(void);
 void rmh_free(void* p);
+/* "burn_raymarching_amd host 0.1.0 src <16 hex>": the sha256 prefix of the host library's sources
+ * (csrc/host/{io,data,driver,comm}.cpp, rmh_common.hpp, rm_host.h, raymarch.h), compiled in by
+ * _build.py, so that a shipped librm_host.so names the tree it came from (rm_version() does the
+ * same for libraymarch_hip.so). */
+const char* rmh_version(void);
 
 /* ---- util.rs: images ----------------------------------------------------------------- */
 /* 8-bit PNG (grey, grey+alpha, RGB, RGBA, palette; non-interlaced) -> RGB8 [h][w][3]. */

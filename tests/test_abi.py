@@ -97,3 +97,19 @@ def test_shipped_library_matches_sources(native):
     want = _build.source_hash()
     assert native.lib().rm_version().decode().endswith("src " + want)
     assert _build.lib_source_hash(native.LIB_PATH) == want
+
+
+def test_shipped_host_binaries_match_sources():
+    """librm_host.so and rm_train (they also travel prebuilt to the GPU box) carry the sha256
+    prefix of the sources they were built from, as libraymarch_hip.so does (_build.py)."""
+    import subprocess
+    from burn_raymarching_amd import _build, host
+    if os.environ.get("RM_LIB_PATH") or os.environ.get("RMH_LIB_PATH"):
+        pytest.skip("RM_LIB_PATH / RMH_LIB_PATH name other libraries")
+    want_host = _build.source_hash(_build.HOST_SOURCES)
+    assert _build.lib_source_hash(_build.HOST_LIB, _build.HOST_TAG) == want_host
+    assert host.lib().rmh_version().decode().endswith("src " + want_host)
+    want_exe = _build.source_hash(_build.EXE_SOURCES)
+    assert _build.lib_source_hash(_build.EXE, _build.EXE_TAG) == want_exe
+    out = subprocess.run([_build.EXE, "--version"], capture_output=True, text=True, check=True).stdout.split("\n")
+    assert out[0] == "rm_train src " + want_exe and out[1].endswith("src " + want_host), out

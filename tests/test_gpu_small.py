@@ -468,3 +468,118 @@ def test_train_step_sampled_prepared(rm, oracle, monkeypatch, m, nu, nf, mode):
         for name, u, v in zip(names, xa, xb):
             assert torch.equal(u, v), (it, name, (u - v).abs().max().item())
     assert a[-1][5][1] > 0  # the penalty share was written
+
+
+def _f16_steps(torch, native, render, model, src, fg, nu, nf, sc, steps, monkeypatch, prepare):
+    """`steps` data-parallel steps of an fp16-colour model (configs[4]'s colour format):
+    rm_train_step_sampled_prepared -> rm_optimizer_step_f16 (colors_f16_out: the next render's
+    colours); prepare False runs the same calls with RM_OPT_PREPARE=0 (the full optimizer)."""
+    import ctypes
+    monkeypatch.setenv("RM_OPT_PREPARE", "1" if prepare else "0")
+    m = sc["centers"].shape[0]
+    sm = model.SceneModel.from_activated(sc["centers"], sc["colors"], sc["radius"], sc["light_dir"], sc["ambient"])
+    raw = sm.raw.clone()
+    act = sm.activated_packed().clone()
+    col_h = act[3 * m:6 * m].half().contiguous()
+    npk = model.packed_size(m)
+    grad = torch.zeros(npk, device="cuda")
+    mom = [torch.zeros(npk, device="cuda") for _ in range(2)]
+    loss = torch.zeros(2, device="cuda")
+    ctx = render.context()
+    p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    o, d, t = src
+    n = nu + nf
+    out = []
+    for it in range(1, steps + 1):
+        march = native.march_params(40, 5.0 + 27.0 * it / steps)
+        march.flags |= native.RM_MARCH_COLOR_F16
+        s = native.RmScene()
+        ctx._lib.rm_scene_from_packed(p(act), m, ctypes.byref(s))
+        s.colors = col_h.data_ptr()
+        g = native.RmGrads()
+        ctx._lib.rm_grads_from_packed(p(grad), m, ctypes.byref(g))
+        ctx.check(ctx._lib.rm_train_step_sampled_prepared(ctx.handle, p(o), p(d), p(t), o.shape[0], p(fg), fg.numel(),
+                                                          nu, nf, 13, 1, it, it / steps, 1.0 / (3 * n), ctypes.byref(s),
+                                                          ctypes.byref(march), ctypes.byref(g), p(loss), p(raw), it, 1,
+                                                          ctypes.c_void_p(loss.data_ptr() + 4)),
+                  "rm_train_step_sampled_prepared")
+        ctx.check(ctx._lib.rm_optimizer_step_f16(ctx.handle, p(raw), p(grad), p(mom[0]), p(mom[1]), m, it, 0.01, 1e-5,
+                                                 1, ctypes.c_void_p(loss.data_ptr() + 4), p(act), p(col_h)),
+                  "rm_optimizer_step_f16")
+        out.append([x.clone() for x in (raw, act, col_h, grad, mom[0], mom[1], loss)])
+    torch.cuda.synchronize()
+    return out
+
+
+@pytest.mark.parametrize("m", [7, 24])
+def test_train_step_sampled_prepared_color_f16(rm, oracle, monkeypatch, m):
+    """The multi-rank driver's prepared step on an fp16-colour model (configs[4] growth runs:
+    rm_optimizer_step_f16 -> rm_optimizer_post_small with colors_f16_out) equals the full optimizer
+    (RM_OPT_PREPARE=0) bit for bit: raw parameters, moments, activated values, the fp16 colours
+    of the next render, gradient and losses, over five steps."""
+    import torch
+    render, model, native = rm
+    cams = model.ring_cameras(4)
+    rays = [oracle.camera_rays(64, 64, *c, precision="f32") for c in cams]
+    o = np.concatenate([r[0] for r in rays])
+    d = np.concatenate([r[1] for r in rays])
+    tg = oracle.render_diff(o.astype(np.float64), d.astype(np.float64), train_scene(model, 6, 2), 24, 32.0)
+    src = [dev(o), dev(d), dev(tg)]
+    fg = torch.from_numpy(np.flatnonzero(tg.sum(1) > 0.01).astype(np.int32)).cuda()
+    sc = train_scene(model, m, 90 + m)
+    a = _f16_steps(torch, native, render, model, src, fg, 13107, 3277, sc, 5, monkeypatch, True)
+    b = _f16_steps(torch, native, render, model, src, fg, 13107, 3277, sc, 5, monkeypatch, False)
+    names = ("raw", "act", "colors_f16", "grad", "adam_m", "adam_v", "loss")
+    for it, (xa, xb) in enumerate(zip(a, b)):
+        for name, u, v in zip(names, xa, xb):
+            assert torch.equal(u, v), (it, name, (u.float() - v.float()).abs().max().item())
+    assert a[-1][6][1] > 0
+
+
+def test_prepared_step_dropped_by_another_call(rm, oracle, monkeypatch):
+    """A preparation is dropped by any other library call before the optimizer step:
+    prepare on the parameters, change them on the host side and call rm_scene_activate, then
+    rm_optimizer_step -- it must compute on the changed parameters (equal to RM_OPT_PREPARE=0 with
+    the same change), not apply the factors prepared on the old ones."""
+    import ctypes
+    import torch
+    render, model, native = rm
+    m, nu, nf = 7, 6000, 2000
+    cams = model.ring_cameras(2)
+    rays = [oracle.camera_rays(48, 48, *c, precision="f32") for c in cams]
+    o = dev(np.concatenate([r[0] for r in rays]))
+    d = dev(np.concatenate([r[1] for r in rays]))
+    tg = dev(np.random.default_rng(5).uniform(size=(o.shape[0], 3)))
+    fg = torch.arange(0, o.shape[0], 2, dtype=torch.int32, device="cuda")
+    sc = train_scene(model, m, 123)
+    p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    res = []
+    for prepare in ("1", "0"):
+        monkeypatch.setenv("RM_OPT_PREPARE", prepare)
+        ctx = render.context()
+        sm = model.SceneModel.from_activated(sc["centers"], sc["colors"], sc["radius"], sc["light_dir"], sc["ambient"])
+        raw = sm.raw.clone()
+        act = sm.activated_packed().clone()
+        npk = model.packed_size(m)
+        grad = torch.zeros(npk, device="cuda")
+        mom = [torch.zeros(npk, device="cuda") for _ in range(2)]
+        loss = torch.zeros(2, device="cuda")
+        s = native.RmScene()
+        ctx._lib.rm_scene_from_packed(p(act), m, ctypes.byref(s))
+        g = native.RmGrads()
+        ctx._lib.rm_grads_from_packed(p(grad), m, ctypes.byref(g))
+        march = native.march_params(40, 20.0)
+        ctx.check(ctx._lib.rm_train_step_sampled_prepared(ctx.handle, p(o), p(d), p(tg), o.shape[0], p(fg), fg.numel(),
+                                                          nu, nf, 3, 1, 1, 0.5, 1.0 / (3 * (nu + nf)), ctypes.byref(s),
+                                                          ctypes.byref(march), ctypes.byref(g), p(loss), p(raw), 1, 1,
+                                                          ctypes.c_void_p(loss.data_ptr() + 4)),
+                  "rm_train_step_sampled_prepared")
+        torch.cuda.synchronize()
+        raw.add_(0.25)  # a host-side change of the parameters (e.g. a broadcast) between the calls
+        ctx.check(ctx._lib.rm_scene_activate(ctx.handle, p(raw), m, p(act)), "rm_scene_activate")
+        ctx.check(ctx._lib.rm_optimizer_step(ctx.handle, p(raw), p(grad), p(mom[0]), p(mom[1]), m, 1, 0.01, 1e-5, 1,
+                                             ctypes.c_void_p(loss.data_ptr() + 4), p(act)), "rm_optimizer_step")
+        torch.cuda.synchronize()
+        res.append([x.clone() for x in (raw, act, mom[0], mom[1], loss)])
+    for name, u, v in zip(("raw", "act", "adam_m", "adam_v", "loss"), *res):
+        assert torch.equal(u, v), (name, (u - v).abs().max().item())

@@ -1,0 +1,39 @@
+"""The reference loop's whole trajectory, pinned bit for bit.
+
+rm_train train runs train.rs:138-208 (5 stages x 700 steps, prune_and_split between stages, k
+annealed 5 -> 32) on the reference's ten poses and target PNGs with seed 0. Its final sphere
+count, final loss bits and the sha256 of the exported scene.json (every parameter bit) are
+committed in tests/golden/rm_train_trajectory.json (tools/pin_trajectory.py). The prune/split
+schedule amplifies any rounding change anywhere in the step -- sampler, march, backward, final
+reduction, penalties, Adam -- so a kernel edit that was meant to be bit-identical and is not fails
+here instead of passing every tolerance test. One process (rm_train_iteration: one launch per
+step) and --ranks 1 (rm_train_step_sampled_prepared, the RCCL all-reduce, the update-only
+optimizer) must both reproduce it.
+"""
+import json
+import os
+import sys
+
+import pytest
+
+from conftest import GOLDEN, gpu_available
+
+pytestmark = pytest.mark.gpu
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+
+
+@pytest.fixture(scope="module")
+def pin():
+    if not gpu_available():
+        pytest.skip("no GPU")
+    with open(os.path.join(GOLDEN, "rm_train_trajectory.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("ranks", [0, 1])
+def test_rm_train_trajectory_is_pinned(pin, ranks):
+    import pin_trajectory
+    got = pin_trajectory.run(ranks)
+    for k in ("num_spheres", "final_loss_bits", "scene_sha256"):
+        assert got[k] == pin[k], (k, got, pin)
