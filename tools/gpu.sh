@@ -58,6 +58,31 @@ benchab)
         $O/${C}_${v}_$r.json $C $v
     done
   done | tee -a $O/ab.txt ;;
+envab)
+  # envab <tag> <n> <config> <ENV=V|-> ... -- <bench args>: bench.py per environment setting
+  # (- = none), alternating, n rounds. {G} in the bench args = gpurun_out/<tag>/grown (see grow)
+  N=$1; C=$2; shift 2; ENVS=()
+  while [ "$1" != "--" ]; do ENVS+=("$1"); shift; done; shift
+  ARGS=$(echo "$@" | sed "s#{G}#$O/grown#g")
+  for r in $(seq $N); do
+    for e in "${ENVS[@]}"; do
+      tagv=$(echo "$e" | tr -c 'A-Za-z0-9_\n' '_')
+      if [ "$e" = - ]; then e="RM_NOOP=1"; fi
+      env $e timeout -k 10 300 python bench.py --cpu-baseline off $ARGS > $O/${C}_${tagv}_$r.json 2> $O/${C}_${tagv}_$r.err \
+        || { tail $O/${C}_${tagv}_$r.err; exit 1; }
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); r=d['roofline']; print(sys.argv[2], sys.argv[3], d['value'], d['ms_per_step'], r['kernel_ms_per_step'], r['frac'], r['executed_frac'])" \
+        $O/${C}_${tagv}_$r.json $C "$e"
+    done
+  done | tee -a $O/ab.txt ;;
+grow)
+  # configs[4]'s grown model (tools/gpu_configs.sh grow): generate.rs targets at 512x512 on the
+  # cameras.json poses, then 11 x 100 steps of prune_and_split growth to 4096 spheres, fp16 colours
+  G=$O/grown; mkdir -p $G/data
+  timeout -k 10 120 $L/rm_train generate --out $G/data --prefix "" --size 512x512 > $G/generate.log 2>&1 && \
+  timeout -k 10 600 $L/rm_train train --cameras $G/data/cameras.json --out $G --size 512x512 \
+    --march-steps 128 --color-f16 --stages 11 --steps 100 --split-all --max-spheres 4096 \
+    --log-every 100 --no-previews > $G/train.log 2>&1 || { tail $G/train.log; exit 1; }
+  grep -E "Next N|num_spheres" $G/train.log | tail -3 ;;
 round) bash tools/gpu_round.sh $TAG "$@" ;;
 configs) bash tools/gpu_configs.sh $TAG "$@" ;;
 *) echo "unknown recipe $RECIPE"; exit 2 ;;
