@@ -37,3 +37,16 @@ def test_rm_train_trajectory_is_pinned(pin, ranks):
     got = pin_trajectory.run(ranks)
     for k in ("num_spheres", "final_loss_bits", "scene_sha256"):
         assert got[k] == pin[k], (k, got, pin)
+
+
+def test_growth_trajectory_is_pinned(pin, tmp_path):
+    """BASELINE configs[4] as stated, grown 7 -> 4096 spheres at 512x512 / 128 steps / fp16 colours
+    (tools/gpu_configs.sh grow): the general kernel, the split march with its continuation
+    launches, the fp16 optimizer and the growth knobs of prune_and_split, pinned bit for bit like
+    the reference loop."""
+    import pin_trajectory
+    if "growth" not in pin:
+        pytest.fail("tests/golden/rm_train_trajectory.json has no growth pin (tools/pin_trajectory.py --write)")
+    got = pin_trajectory.run(0, 100, extra=pin_trajectory.GROWTH, cams=pin_trajectory.generate(str(tmp_path)))
+    for k in ("num_spheres", "final_loss_bits", "scene_sha256"):
+        assert got[k] == pin["growth"][k], (k, got, pin["growth"])
