@@ -232,6 +232,22 @@ struct KArgs {
   int cont_stride;   // entries per class list
   int cont_order;    // 0: every deferred block in class 0 (arrival order)
   long long cont_rays;
+  // Ray mode (split launches; RM_RAY_MODE): every march step takes the scene-uniform fixed shift
+  // (the running maximum where the scene does not admit it), so a ray's step is a function of its
+  // own state alone. Then a ray whose t repeats with period 2 retires with its final t by itself
+  // (the wave-level cycle exit generalised), and at a continuation cap the still-marching RAYS,
+  // not their groups, go on: the group saves every ray's state (cont_state gets an eighth per-ray
+  // row, the ray's choice history), appends itself to cont_list_w (class 0) and its marching rays
+  // to ray_list_w. A ray_cont launch marches 32 listed rays per block (ray_list[0..*ray_count),
+  // any groups) from cont_resume to its cap or to the end and writes their states back; the
+  // groups' post-march forward and backward then run in a resume launch (cont_resume = steps).
+  // The grouping of rays changes no bit.
+  int ray_mode;
+  int ray_cont;
+  const int* ray_list;
+  const int* ray_count;
+  int* ray_list_w;
+  int* ray_count_w;
 #ifdef RM_BLOCK_TRACE
   unsigned long long* btrace;  // measurement build: per-wave timing records (rm_ray_kernel)
 #endif
@@ -1656,7 +1672,19 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   int cls = -1;  // the block's cost class in the previous launch (cost-ordered dispatch), else -1
   long long blk;
-  if (SPLIT && a.cont_resume > 0) {  // continuation launch: the blocks the first launch deferred
+  // ray_cont (ray mode): this block marches listed rays [32 b, 32 b + 32) of ray_list, one per lane
+  // (lanes l and l + 32 the same ray); lanes past the list's end are invalid copies of its first
+  long long li_listed = -1;
+  bool listed = true;
+  if (SPLIT && a.cont_resume > 0 && a.ray_cont) {
+    const int n = *a.ray_count;
+    const int i0 = (int)blockIdx.x * kSplitRays;
+    if (i0 >= n) return;
+    const int i = i0 + (lane & (kSplitRays - 1));
+    listed = i < n;
+    li_listed = a.ray_list[listed ? i : i0];
+    blk = -1;  // no group of its own
+  } else if (SPLIT && a.cont_resume > 0) {  // continuation launch: the blocks the first launch deferred
     // position blockIdx.x of the class-major concatenation of the class lists
     int b = (int)blockIdx.x, c = 0;
     for (; c < kContClasses; ++c) {
@@ -1670,13 +1698,14 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     blk = ray_block(a, &cls);
   }
   // SPLIT: lane l holds ray l mod kSplitRays of the group (kSplitRays < 64: copies, see kSplitRays)
-  const long long li = SPLIT ? blk * kSplitRays + (lane & (kSplitRays - 1)) : blk * kBlock + tid;
+  const long long li = li_listed >= 0 ? li_listed
+                                      : (SPLIT ? blk * kSplitRays + (lane & (kSplitRays - 1)) : blk * kBlock + tid);
 #if RM_HEAVY_PRIO
   // the dearest class's waves first at the SIMD's issue arbiter: they set the launch's critical
   // path, the cheaper waves fill the issue slots they leave
   if (cls >= 0 && cls < RM_HEAVY_PRIO) __builtin_amdgcn_s_setprio(2);
 #endif
-  const bool valid = li < a.n_rays;
+  const bool valid = listed && li < a.n_rays;
   long long ri = a.ray_begin + (valid ? li : 0);  // becomes the ray's row in the [N,3] tensors
   // the wave that writes this ray's outputs; SPLIT: all four waves run the post-march forward
   // (each over a quarter of the spheres, merged) and wave w seeds the backward of the group's rays
@@ -1695,7 +1724,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   // (rm_escape_kernel) gets out = 0 and zero gradients without marching -- exactly what the full
   // computation yields for them, since their silhouette mask is 0 in f32 (see escapes()).
   if (a.ocnt_z != nullptr && blockIdx.x == 0 && tid < RM_ORDER_CLASSES) order_sets(a).cnt_z[tid * RM_ORDER_CLS_STRIDE] = 0;
-  if (a.esc_flags != nullptr && a.esc_flags[blk]) {
+  if (a.esc_flags != nullptr && blk >= 0 && a.esc_flags[blk]) {
     if (a.stats != nullptr && tid == 0) atomicAdd(a.stats, 1ull);
     if (a.ocnt_w != nullptr && tid == 0) order_append(a, blk, 0);
     escaped_block<MODE>(a, L, blk, ri, valid, tid, lane, wave);
@@ -1726,6 +1755,8 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   // Rays proven to escape (`gone`, see the march) no longer take part in the wave-uniform
   // choices: their outputs and gradient terms are exactly 0 whatever they compute.
   bool gone = false;
+  // Ray mode: the ray's state repeats with period 2; its t is final (see the march)
+  bool retired = false;
   // A second proof per ray (camera mode): rho_lb, a lower bound on the distance to the nearest
   // sphere CENTRE -- the eye's (write_origins), less the path marched since (every centre distance
   // is 1-Lipschitz along the ray). Where the soft-min runs far below the hard min (small k: at
@@ -1822,14 +1853,17 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   unsigned long long tr_paths = 0, tr_lse_cyc = 0, tr_vec = 0;
 #endif
   // choice: the step's wave-uniform choices, bit 0 unshifted, bit 1 fixed shift, bit 2 clamp-free
-  auto soft_min_march = [&](const float p[3], bool fast, float Dprev, int& choice) {
-    bool none = shift_none_ok && __all(2.0f * fmaxf(Dprev, 0.0f) + a.lse_slack <= 90.0f * inv_kappa || gone);
+  // force: 0 the cheapest safe shift for the wave (above); 1 the fixed shift, 2 the running maximum
+  // (ray mode: see soft_min_march)
+  auto soft_min_core = [&](const float p[3], bool fast, float Dprev, int& choice, int force) {
+    bool none = force == 0 && shift_none_ok &&
+                __all(2.0f * fmaxf(Dprev, 0.0f) + a.lse_slack <= 90.0f * inv_kappa || gone);
     // or: the nearest sphere is no farther than sphere 0, k (rho_0 - r_0) = rho'_0 - k r_0 <= 90
     // bounds k d_min just as well (the first steps after the eye, where the 2 D bound is loose)
-    if (!none && shift_none_ok && a.mfma)
+    if (!none && force == 0 && shift_none_ok && a.mfma)
       none = __all(fixed_shift(p, kappa * kappa, Lds::v4(L.S0[0]), Lds::v4(L.S1[0])) - kr_first <= 90.0f || gone);
     float m = none ? 0.0f : -INFINITY, s = 0.0f;
-    const bool fixed = !none && shift_fixed_ok && __all(psq(p) <= 1e10f || gone);
+    const bool fixed = force == 1 || (force == 0 && !none && shift_fixed_ok && __all(psq(p) <= 1e10f || gone));
     choice = (none ? 1 : 0) | (fixed ? 2 : 0) | (fast ? 4 : 0);
     if ((none || fixed) && a.mfma) {
       const float k2 = kappa * kappa;
@@ -1901,6 +1935,26 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     }
     return -(flog2(fmaxf(s, 1e-30f)) + m) * inv_kappa;
   };
+  // The march's soft-min. Ray mode (the split kernels): each ray's own choice, so that its step is
+  // a function of its own state -- the scene-uniform fixed shift for every ray whose |p| admits it
+  // (|p| <= 1e5, the fixed form's fp32 headroom), the running maximum (a vector sweep over all
+  // spheres, lane by lane) for the others and when the scene admits no fixed shift; a wave runs
+  // the maximum's sweep only when one of its live rays needs it.
+  auto soft_min_march = [&](const float p[3], bool fast, float Dprev, int& choice) {
+    if constexpr (SPLIT) {
+      const bool far = !gone && !retired && !(psq(p) <= 1e10f);
+      const bool any_far = __ballot(far) != 0ull;
+      int cm = 0;
+      float Dm = 0.0f, Dx = 0.0f;
+      if (shift_fixed_ok) Dm = soft_min_core(p, fast, Dprev, cm, 1);
+      if (!shift_fixed_ok || any_far) Dx = soft_min_core(p, fast, Dprev, cm, 2);
+      const bool use_fixed = shift_fixed_ok && !far;
+      choice = (use_fixed ? 2 : 0) | (fast ? 4 : 0);
+      return use_fixed ? Dm : Dx;
+    } else {
+      return soft_min_core(p, fast, Dprev, choice, 0);
+    }
+  };
 
   // ---- march: t <- (t + sdf(o + d t)).detach(), S times (renderer_diff.rs:20-26)
   // The fast path needs a distance lower bound: the previous point's hard minimum (>= its
@@ -1952,7 +2006,7 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       const float ex = p[0] - c0x, ey = p[1] - c0y, ez = p[2] - c0z;
       const float Tn = esc_tab[min(a.steps - st, kEscTab - 1)];
       const float dist = fsqrt(fmaf(ez, ez, fmaf(ey, ey, ex * ex)));
-      gone = gone || (fmaf(ez, d[2], fmaf(ey, d[1], ex * d[0])) >= 0.0f && dist * (1.0f - 1e-5f) >= Tn);
+      gone = gone || (!retired && fmaf(ez, d[2], fmaf(ey, d[1], ex * d[0])) >= 0.0f && dist * (1.0f - 1e-5f) >= Tn);
       gone_step = dist - rprime;
       if (a.early_exit && __all(gone || !valid)) {
         steps_saved += a.steps - st;
@@ -1964,6 +2018,18 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
 #endif
       return false;
     };
+    // A gone ray's remaining bound steps from step `from` to the end (what the march would do):
+    // where the march of its wave stops early but its rays' final states are used later (ray mode:
+    // the continuation caps and the listed rays' write-back) -- a gone ray's mask is exactly 0
+    // only where the bound steps end, not where it was proven
+    auto gone_finish = [&](int from) {
+      if (gone && !retired)
+        for (int k = from; k < a.steps; ++k) {
+          const float q[3] = {fmaf(d[0], t, o[0]) - c0x, fmaf(d[1], t, o[1]) - c0y, fmaf(d[2], t, o[2]) - c0z};
+          t = fminf(t + (fsqrt(fmaf(q[2], q[2], fmaf(q[1], q[1], q[0] * q[0]))) - rprime), kTMax);
+        }
+    };
+    int st_stop = -1;  // the step at which the march found every ray of the wave gone (not taken)
     int st0 = 0;
 #ifdef RM_BLOCK_TRACE
     const unsigned long long tr_c_begin = __builtin_readcyclecounter();
@@ -2001,52 +2067,63 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     float cyc_t4 = __builtin_nanf("");
 #endif
     int chist = 0xFFF;
+    int rhist = 0xFFF;  // ray mode: the ray's own choice history (per lane: listed rays come from many groups)
     static_assert(RM_CYCLE_MAX == 2 || !SPLIT, "the continuation saves two steps of history");
     if (SPLIT && a.cont_resume > 0) {  // the state the first launch saved at step cont_resume
       const float* cs = a.cont_state;
       const long long R = a.cont_rays;
+      const long long G = (SPLIT ? 8 : 7) * R;  // the per-group words after the per-ray rows
       t = cs[li];
       lb = cs[R + li];
       Dprev = cs[2 * R + li];
       cyc_t1 = cs[3 * R + li];
       cyc_t2 = cs[4 * R + li];
-      gone = cs[5 * R + li] != 0.0f;
+      const float gflag = cs[5 * R + li];  // ray mode: 1 gone, 2 retired; else non-zero = gone
+      gone = SPLIT ? gflag == 1.0f : gflag != 0.0f;
+      retired = SPLIT && gflag == 2.0f;
       rho_lb = cs[6 * R + li];
-      chist = __float_as_int(cs[7 * R + 2 * blk]);
-      steps_saved = __float_as_int(cs[7 * R + 2 * blk + 1]);
+      if (SPLIT) rhist = __float_as_int(cs[7 * R + li]);
+      if (!a.ray_cont) {
+        chist = __float_as_int(cs[G + 2 * blk]);
+        steps_saved = __float_as_int(cs[G + 2 * blk + 1]);
+      }
       st0 = a.cont_resume;
     }
+    const unsigned long long below = (1ull << lane) - 1ull;
     for (int st = st0; !dead && st < a.steps; ++st) {
-      if (SPLIT && a.cont_cap > 0 && st == a.cont_cap) {  // defer: save the state at the top of this step
-        // the block's class: the march steps its slowest ray still needs, predicted from its last
-        // two steps as a linear convergence (the next step ~ rho times the last; grazing rays have
-        // rho near 1) down to a few ulp of t, where the cycle exit takes it; gone rays need none
-        float need = 0.0f;
-        if (lane < kSplitRays && valid && !gone) {
-          const float d1 = fabsf(t - cyc_t1), d0 = fabsf(cyc_t1 - cyc_t2);
-          const float tiny = 4.0f * fmaxf(fabsf(t), 1e-3f) * 1.2e-7f;
-          if (d1 > tiny) {
-            const float rho = d0 > 0.0f ? d1 / d0 : 1.0f;
-            need = (rho >= 0.97f || !(rho == rho)) ? 1e9f : flog2(d1 / tiny) / -flog2(rho);
-          }
-        }
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) need = fmaxf(need, __shfl_xor(need, off));
-        const int cls = !a.cont_order ? 0 : (need >= 60.0f ? 0 : (need >= 30.0f ? 1 : (need >= 10.0f ? 2 : 3)));
-        if (wave == 0 && lane < kSplitRays) {  // the four waves (and a ray's copies) hold the same state
-          float* cs = a.cont_state;
-          const long long R = a.cont_rays;
+      if (SPLIT && a.cont_cap > 0 && st == a.cont_cap) {
+        // ray mode, defer at the top of this step: every ray's state, the marching rays to the
+        // ray list; a group (not a ray_cont block) also to the resume list, its not-run steps
+        // counted as saved now (the ray_cont blocks subtract the steps they run)
+        float* cs = a.cont_state;
+        const long long R = a.cont_rays;
+        const bool act = valid && !gone && !retired && lane < kSplitRays;
+        gone_finish(st);
+        if (wave == 0 && lane < kSplitRays && valid) {
           cs[li] = t;
           cs[R + li] = lb;
           cs[2 * R + li] = Dprev;
           cs[3 * R + li] = cyc_t1;
           cs[4 * R + li] = cyc_t2;
-          cs[5 * R + li] = gone ? 1.0f : 0.0f;
+          cs[5 * R + li] = gone ? 1.0f : (retired ? 2.0f : 0.0f);
           cs[6 * R + li] = rho_lb;
+          cs[7 * R + li] = __int_as_float(rhist);
+        }
+        if (wave == 0) {
+          const unsigned long long am = __ballot(act);
+          const int na = __popcll(am);
+          int base = 0;
+          if (lane == 0 && na > 0) base = atomicAdd(a.ray_count_w, na);
+          base = __shfl(base, 0);
+          if (act) a.ray_list_w[base + __popcll(am & below)] = (int)li;
           if (lane == 0) {
-            cs[7 * R + 2 * blk] = __int_as_float(chist);
-            cs[7 * R + 2 * blk + 1] = __int_as_float(steps_saved);
-            a.cont_list_w[(long long)cls * a.cont_stride + atomicAdd(a.cont_count_w + cls, 1)] = (int)blk;
+            if (!a.ray_cont) {
+              cs[8 * R + 2 * blk] = __int_as_float(chist);
+              cs[8 * R + 2 * blk + 1] = __int_as_float(steps_saved + (a.steps - st));
+              a.cont_list_w[atomicAdd(a.cont_count_w, 1)] = (int)blk;
+            } else if (a.stats != nullptr && st > st0) {
+              atomicAdd(a.stats + 2, (unsigned long long)(-(long long)(st - st0)));
+            }
           }
         }
         return;
@@ -2057,11 +2134,52 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       const float p[3] = {fmaf(d[0], t, o[0]), fmaf(d[1], t, o[1]), fmaf(d[2], t, o[2])};
       if (wave_escaped(st, p)) {
         dead = true;
+        st_stop = st;
         break;
       }
       int choice;
       const float D = soft_min_march(p, all_safe(lb, rho_lb), Dprev, choice);
       const float t_step = t;  // this step's state: (t_step, choice)
+      if constexpr (SPLIT) {
+        // Ray mode: a ray's step is a function of its own t (the shift is scene-uniform; the clamp
+        // choice changes no bit), so a ray whose t repeats with period 2 (t_step == t two steps
+        // back, under the same shift choice) keeps repeating: it retires with the state the march
+        // would end in -- this step's when an even number of steps is left, the next one's
+        // otherwise -- and keeps it (its lanes still run, their results unused). Gone rays
+        // (sticky) and retired rays leave the wave-uniform choices.
+        const float rl0 = rho_lb;
+        if (!retired) {
+          t = fminf(t + (gone ? gone_step : D), kTMax);
+          rho_lb = rho_moved(rl0, t_step, t);
+          lb = D - fabsf(D);
+          Dprev = D;
+        }
+        if (a.early_exit && MODE != kRender) {
+          if (!retired && !gone && valid && t_step == cyc_t2 && (choice & 3) == ((rhist >> 3) & 3)) {
+            retired = true;
+            if (((a.steps - st) & 1) == 0) {  // the state after the last step is this step's
+              t = t_step;
+              rho_lb = rl0;
+            }
+          }
+          if (!retired) {
+            cyc_t2 = cyc_t1;
+            cyc_t1 = t_step;
+          }
+          rhist = ((rhist << 3) | choice) & 0xFFF;
+          if (__all(gone || !valid || retired)) {  // every ray final or gone: gone rays take their bound steps
+            if (gone) {
+              for (int k = st + 1; k < a.steps; ++k) {
+                const float q[3] = {fmaf(d[0], t, o[0]) - c0x, fmaf(d[1], t, o[1]) - c0y, fmaf(d[2], t, o[2]) - c0z};
+                t = fminf(t + (fsqrt(fmaf(q[2], q[2], fmaf(q[1], q[1], q[0] * q[0]))) - rprime), kTMax);
+              }
+            }
+            steps_saved += a.steps - 1 - st;
+            break;
+          }
+        }
+        continue;
+      }
       t = fminf(t + (gone ? gone_step : D), kTMax);
       rho_lb = rho_moved(rho_lb, t_step, t);
       // next point: hard min >= soft-min D here, moved by |D|
@@ -2122,6 +2240,23 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
         cyc_t1 = t_step;
         chist = ((chist << 3) | choice) & 0xFFF;
       }
+    }
+    if (SPLIT && a.ray_cont) {
+      // ray mode: the listed rays' final states back into their groups' rows (the resume launch
+      // runs the groups' post-march forward and backward); the steps this block ran uncounted
+      // from the saved steps its groups booked at the cap
+      float* cs = a.cont_state;
+      const long long R = a.cont_rays;
+      if (st_stop >= 0) gone_finish(st_stop);
+      if (wave == 0 && lane < kSplitRays && valid) {
+        cs[li] = t;
+        cs[R + li] = lb;
+        cs[5 * R + li] = gone ? 1.0f : (retired ? 2.0f : 0.0f);
+        cs[6 * R + li] = rho_lb;
+      }
+      const long long run = (long long)(a.steps - st0) - steps_saved;
+      if (wave == 0 && lane == 0 && a.stats != nullptr && run > 0) atomicAdd(a.stats + 2, (unsigned long long)(-run));
+      return;
     }
   RM_TRACE(4, __builtin_amdgcn_s_memrealtime());
   RM_TRACE(6, (unsigned long long)steps_saved);
@@ -3781,6 +3916,13 @@ int split_cont_caps(int steps, int (&caps)[kMaxCont + 1]) {
       while (*q && *q != ',') ++q;
       if (*q == ',') ++q;
     }
+  } else if (steps >= 128 && !std::getenv("RM_SPLIT_CONT_STEPS") && !std::getenv("RM_SPLIT_CONT2_STEPS")) {
+    // ray mode: a continuation costs only the rays still marching, so defer earlier and more
+    // often -- 3S/16, 3S/8, 3S/4 (C5g, one box: 24 / 48 / 96 of 128 steps 42.3 Mrays/s against 39.8
+    // with 48 / 96 and 40.1 with 32 / 96; 16 / 32 / 64 / 96 42.3; C5 within 1 %, profiles/r07g)
+    caps[n++] = 3 * steps / 16;
+    caps[n++] = 3 * steps / 8;
+    caps[n++] = 3 * steps / 4;
   } else {
     const int c0 = split_cont_steps(steps), c1 = split_cont2_steps(steps);
     if (c0 > 0 && c0 < steps) {
@@ -4256,6 +4398,9 @@ int run(rm_context* ctx, const Call& c) {
       split = (M >= kSplitMinSpheres && n_all <= kSplitMaxRays) || (M >= kSplitMinSpheresWide && n_all <= kSplitMaxRaysWide);
   }
   a.split = split ? 1 : 0;
+  // ray mode in every split launch (the scene-uniform shift, per-ray retirement and the ray-level
+  // continuation; the split kernels are compiled for it, KArgs::ray_mode)
+  a.ray_mode = split ? 1 : 0;
   const int rpb = split ? kSplitRays : kBlock;  // rays per block
   a.cull = ((c.march->flags & RM_MARCH_SKIP_ESCAPED) != 0 && mask_vanishes && !c.t_out && !c.dbg && !split) ? 1 : 0;
   a.cull_min_d = c.mode == kRender ? 50.0f : std::max(50.0f, 160.0f / (a.msharp * 1.44269504f));
@@ -4426,10 +4571,16 @@ int run(rm_context* ctx, const Call& c) {
                         a.steps >= 2 * caps[0];
       int* lists[2] = {nullptr, nullptr};
       int* counts[2] = {nullptr, nullptr};
+      const bool rmode = cont && a.ray_mode;
+      int* rlists[2] = {nullptr, nullptr};
+      int* rcounts[2] = {nullptr, nullptr};
       if (cont) {
         const long long rays = nb * kSplitRays;
-        const size_t need = (size_t)(7 * rays + 2 * nb) * sizeof(float) +
-                            (size_t)(2 * kContClasses * nb + 2 * kContClasses + 16) * sizeof(int);
+        // per ray: 7 state rows (8 in ray mode), per group 2 words; the group lists; ray mode: two
+        // ray lists of up to `rays` entries and their counts
+        const size_t need = (size_t)(8 * rays + 2 * nb) * sizeof(float) +
+                            (size_t)(2 * kContClasses * nb + 2 * kContClasses + 16) * sizeof(int) +
+                            (size_t)(2 * rays + 16) * sizeof(int);
         if (ctx->cont_bytes < need) {
           if (ctx->cont_buf) RM_HIP(ctx, hipFree(ctx->cont_buf));
           ctx->cont_buf = nullptr;
@@ -4437,10 +4588,14 @@ int run(rm_context* ctx, const Call& c) {
           RM_HIP(ctx, hipMalloc(&ctx->cont_buf, need));
           ctx->cont_bytes = need;
         }
-        lists[0] = reinterpret_cast<int*>(ctx->cont_buf + 7 * rays + 2 * nb);
+        lists[0] = reinterpret_cast<int*>(ctx->cont_buf + 8 * rays + 2 * nb);
         lists[1] = lists[0] + kContClasses * nb;
         counts[0] = lists[1] + kContClasses * nb;
         counts[1] = counts[0] + kContClasses;
+        rcounts[0] = counts[1] + kContClasses;
+        rcounts[1] = rcounts[0] + 8;  // a 32-byte line each
+        rlists[0] = rcounts[1] + 8;
+        rlists[1] = rlists[0] + rays;
         a.cont_state = ctx->cont_buf;
         a.cont_rays = rays;
         a.cont_list_w = lists[0];
@@ -4450,23 +4605,54 @@ int run(rm_context* ctx, const Call& c) {
         a.cont_stride = (int)nb;
         a.cont_order = env_is("RM_CONT_ORDER", '0') ? 0 : 1;
         RM_HIP(ctx, hipMemsetAsync(counts[0], 0, 2 * kContClasses * sizeof(int), ctx->stream));
+        if (rmode) {  // the first launch appends the marching rays to ray list 0
+          a.ray_list_w = rlists[0];
+          a.ray_count_w = rcounts[0];
+          RM_HIP(ctx, hipMemsetAsync(rcounts[0], 0, 16 * sizeof(int), ctx->stream));
+        }
       }
       if (c.mode == kFwd) launch_ray<kFwd>(c.cam, split, grid, lds, ctx->stream, a, ev0, ev1);
       else if (c.mode == kBwd) launch_ray<kBwd>(c.cam, split, grid, lds, ctx->stream, a, ev0, ev1);
       else if (c.mode == kTrain) launch_ray<kTrain>(c.cam, split, grid, lds, ctx->stream, a, ev0, ev1);
       else launch_ray<kRender>(c.cam, false, grid, lds, ctx->stream, a, ev0, ev1);
       RM_HIP(ctx, hipGetLastError());
-      for (int ph = 0; cont && ph < ncaps; ++ph) {
+      // ray mode: continuation k marches the rays of ray list k % 2 (deferring at the next cap into
+      // list (k + 1) % 2, whose count is cleared first: continuation k - 1 read it), then one resume
+      // launch runs the deferred groups' post-march forward and backward from their final states
+      for (int ph = 0; rmode && ph < ncaps; ++ph) {
         KArgs b = a;
+        b.ray_cont = 1;
         b.cont_resume = caps[ph];
-        b.cont_list = lists[ph & 1];
-        b.cont_count = counts[ph & 1];
-        b.cont_cap = caps[ph + 1];  // the next continuation, if any (0: none)
-        b.cont_list_w = lists[(ph + 1) & 1];
-        b.cont_count_w = counts[(ph + 1) & 1];
-        if (ph > 0 && b.cont_cap > 0)  // list (ph + 1) % 2 was read by launch ph - 1: clear its counts
-          RM_HIP(ctx, hipMemsetAsync(b.cont_count_w, 0, kContClasses * sizeof(int), ctx->stream));
-        b.ocnt_z = nullptr;  // cleared by the first launch
+        b.cont_cap = caps[ph + 1];
+        b.ray_list = rlists[ph & 1];
+        b.ray_count = rcounts[ph & 1];
+        b.ray_list_w = rlists[(ph + 1) & 1];
+        b.ray_count_w = rcounts[(ph + 1) & 1];
+        if (b.cont_cap > 0) RM_HIP(ctx, hipMemsetAsync(b.ray_count_w, 0, sizeof(int), ctx->stream));
+        b.cont_list_w = nullptr;
+        b.cont_count_w = nullptr;
+        b.ocnt_z = nullptr;
+        b.olist_r = nullptr;
+        b.ocnt_r = nullptr;
+        b.ocnt_w = nullptr;  // no groups of its own: the resume launch appends them
+        b.olist_w = nullptr;
+        hipEvent_t e0, e1;
+        if ((rc = next_events(ctx, e0, e1)) != RM_OK) return rc;
+        if (c.mode == kBwd) launch_cont<kBwd>(c.cam, grid, lds, ctx->stream, b, e0, e1);
+        else launch_cont<kTrain>(c.cam, grid, lds, ctx->stream, b, e0, e1);
+        RM_HIP(ctx, hipGetLastError());
+      }
+      if (rmode) {
+        KArgs b = a;
+        b.cont_resume = a.steps;
+        b.cont_cap = 0;
+        b.cont_list = lists[0];
+        b.cont_count = counts[0];
+        b.cont_list_w = nullptr;
+        b.cont_count_w = nullptr;
+        b.ray_list_w = nullptr;
+        b.ray_count_w = nullptr;
+        b.ocnt_z = nullptr;
         b.olist_r = nullptr;
         b.ocnt_r = nullptr;
         hipEvent_t e0, e1;

@@ -179,12 +179,13 @@ def test_split_threshold(rm, monkeypatch, m, views, size, split):
 
 
 def test_split_continuation(rm, oracle, monkeypatch):
-    """Continuation launch (split train / backward launches with S >= 64: the blocks still marching
-    at step max(32, 3S/8) stop, and a second launch runs them from their saved march state; from
-    S >= 128 a third from 3S/4):
-    bit-identical to one launch (RM_SPLIT_CONT_STEPS=0), to other continuation steps and to the
-    march with the early exit off; the timed launches show the second launch; the image is within
-    the oracle's tolerance."""
+    """Continuation launches (split train / backward launches with S >= 64; ray mode): at step
+    max(32, 3S/8) the groups still marching stop, their still-marching RAYS go on in a launch that
+    marches 32 listed rays per block (from S >= 128 once more from 3S/4), and a resume launch runs
+    the groups' post-march forward and backward from the rays' final states: bit-identical to one
+    launch (RM_SPLIT_CONT_STEPS=0), to other continuation steps and to the march with the early exit
+    off; the timed launches show first + continuations + resume; the image is within the oracle's
+    tolerance."""
     render, model, native = rm
     W = H = 64
     M, S, K = 300, 64, 32.0
@@ -201,7 +202,7 @@ def test_split_continuation(rm, oracle, monkeypatch):
     base = _train(render, native, cams, W, H, tg, s, K, S)
     ctx.timing(False)
     _, launches = ctx.collect_timing(reset=True)
-    assert launches == 2
+    assert launches == 3
     for steps in ("0", "8", "31", "40"):
         monkeypatch.setenv("RM_SPLIT_CONT_STEPS", steps)
         _equal(base, _train(render, native, cams, W, H, tg, s, K, S))
@@ -212,17 +213,16 @@ def test_split_continuation(rm, oracle, monkeypatch):
     ctx.timing(True)
     _equal(base, _train(render, native, cams, W, H, tg, s, K, S))
     ctx.timing(False)
-    assert ctx.collect_timing(reset=True)[1] == 3
+    assert ctx.collect_timing(reset=True)[1] == 4
     monkeypatch.delenv("RM_SPLIT_CONT2_STEPS")
     _equal(base, _train(render, native, cams, W, H, tg, s, K, S, flags=native.RM_MARCH_NO_EARLY_EXIT))
-    # from S = 128 the default takes the second continuation too (at 3S/4): three launches, the
-    # one launch's bits
+    # from S = 128 the default continues at 3S/16, 3S/8 and 3S/4: five launches, the one launch's bits
     tg2 = render.render_diff_camera(cams, W, H, model.scene_tensors(model.synthetic_scene(M, 24)), K, 128)
     ctx.collect_timing(reset=True)
     ctx.timing(True)
     b128 = _train(render, native, cams, W, H, tg2, s, K, 128)
     ctx.timing(False)
-    assert ctx.collect_timing(reset=True)[1] == 3
+    assert ctx.collect_timing(reset=True)[1] == 5
     monkeypatch.setenv("RM_SPLIT_CONT_STEPS", "0")
     _equal(b128, _train(render, native, cams, W, H, tg2, s, K, 128))
     monkeypatch.delenv("RM_SPLIT_CONT_STEPS")
@@ -232,7 +232,7 @@ def test_split_continuation(rm, oracle, monkeypatch):
     ctx.timing(True)
     _equal(b128, _train(render, native, cams, W, H, tg2, s, K, 128))
     ctx.timing(False)
-    assert ctx.collect_timing(reset=True)[1] == 5
+    assert ctx.collect_timing(reset=True)[1] == 6
     monkeypatch.delenv("RM_SPLIT_CONT_LIST")
     o, d = cam_rays(oracle, cams, W, H)
     check_fwd(base[2].reshape(-1, 3), oracle.render_diff(o.astype(np.float64), d.astype(np.float64), sc, S, K))
@@ -249,11 +249,13 @@ def test_split_continuation(rm, oracle, monkeypatch):
 
 @pytest.mark.parametrize("m", [256, 300, 1100])
 def test_split_costs_no_accuracy(rm, oracle, monkeypatch, m):
-    """The split march's gradient error against the fp64 oracle is the unsplit kernel's: the two
-    differ from each other by at most a quarter of what either differs from the oracle, and both sit below the
-    fp32 reference order's own relative-L2 error at these cases (tools/split_margin.py over 8
-    seeds: split and unsplit worst element 4.32e-2 both at |g| >= 1e-2 max, relL2 <= 3.5e-4 vs the
-    fp32 reference order's 9.4e-4)."""
+    """The split march's gradient error against the fp64 oracle is of the unsplit kernel's order and
+    both sit below the fp32 reference order's own relative-L2 error at these cases. The two march
+    with different soft-min shifts (ray mode: a fixed shift per ray against the unsplit kernel's
+    per-wave choice), so they no longer agree to a fraction of their error; tools/split_margin.py over
+    8 seeds (profiles/r07j_split_margin.jsonl): relL2 split <= 3.7e-4, unsplit <= 3.4e-4, fp32
+    reference order <= 9.4e-4; split / unsplit relL2 <= 1.36, worst element at |g| >= 1e-2 4.2e-2
+    against 4.3e-2."""
     from conftest import PER_SPHERE, grad_errors
     render, model, _ = rm
     W = H = 48
@@ -272,6 +274,7 @@ def test_split_costs_no_accuracy(rm, oracle, monkeypatch, m):
     for key in PER_SPHERE:
         ref = np.asarray(g64[key], np.float64).reshape(-1)
         a, b = got["1"][key].reshape(-1).astype(np.float64), got["0"][key].reshape(-1).astype(np.float64)
-        assert np.abs(a - b).max() <= 0.25 * np.abs(a - ref).max(), key
-        for gg in (a, b):
-            assert grad_errors(gg, ref)[1] <= grad_errors(g32[key], ref)[1], key
+        ea, eb = grad_errors(a, ref)[1], grad_errors(b, ref)[1]
+        assert ea <= 1.5 * eb + 1e-6, key
+        for e in (ea, eb):
+            assert e <= grad_errors(g32[key], ref)[1], key

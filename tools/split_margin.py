@@ -51,6 +51,14 @@ def main():
                 res[name] = {k: v.detach().cpu().numpy() for k, v in got.items()}
             os.environ.pop("RM_SPLIT", None)
             line = {"spheres": m, "seed": seed}
+            for key in ("centers", "colors", "radius"):
+                ref = np.asarray(g64[key], np.float64).reshape(-1)
+                a = res["gpu_split"][key].reshape(-1).astype(np.float64)
+                b = res["gpu_unsplit"][key].reshape(-1).astype(np.float64)
+                # the split / unsplit disagreement as a fraction of the split march's own worst error
+                r = float(np.abs(a - b).max() / max(np.abs(a - ref).max(), 1e-30))
+                line[f"split_vs_unsplit.{key}"] = r
+                summary.setdefault("split_vs_unsplit", []).append(r)
             for name, gr in res.items():
                 for key in ("centers", "colors", "radius"):
                     _, rl2, tiers = grad_errors(gr[key], g64[key])
