@@ -1853,11 +1853,11 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   unsigned long long tr_paths = 0, tr_lse_cyc = 0, tr_vec = 0;
 #endif
   // choice: the step's wave-uniform choices, bit 0 unshifted, bit 1 fixed shift, bit 2 clamp-free
-  // force: 0 the cheapest safe shift for the wave (above); 1 the fixed shift, 2 the running maximum
-  // (ray mode: see soft_min_march)
+  // force: 0 the cheapest safe shift for the wave (above); 1 the fixed shift, 2 the running maximum,
+  // 3 unshifted (ray mode: see soft_min_march)
   auto soft_min_core = [&](const float p[3], bool fast, float Dprev, int& choice, int force) {
-    bool none = force == 0 && shift_none_ok &&
-                __all(2.0f * fmaxf(Dprev, 0.0f) + a.lse_slack <= 90.0f * inv_kappa || gone);
+    bool none = force == 3 || (force == 0 && shift_none_ok &&
+                __all(2.0f * fmaxf(Dprev, 0.0f) + a.lse_slack <= 90.0f * inv_kappa || gone));
     // or: the nearest sphere is no farther than sphere 0, k (rho_0 - r_0) = rho'_0 - k r_0 <= 90
     // bounds k d_min just as well (the first steps after the eye, where the 2 D bound is loose)
     if (!none && force == 0 && shift_none_ok && a.mfma)
@@ -1936,21 +1936,28 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     return -(flog2(fmaxf(s, 1e-30f)) + m) * inv_kappa;
   };
   // The march's soft-min. Ray mode (the split kernels): each ray's own choice, so that its step is
-  // a function of its own state -- the scene-uniform fixed shift for every ray whose |p| admits it
-  // (|p| <= 1e5, the fixed form's fp32 headroom), the running maximum (a vector sweep over all
-  // spheres, lane by lane) for the others and when the scene admits no fixed shift; a wave runs
-  // the maximum's sweep only when one of its live rays needs it.
+  // a function of its own state (its p and previous D) -- unshifted when the ray's own bound admits
+  // it (the tests of soft_min_core, per ray), else the scene-uniform fixed shift when its |p| admits
+  // it (|p| <= 1e5, the fixed form's fp32 headroom), else the running maximum (a vector sweep over
+  // all spheres, lane by lane); a wave runs each form only when one of its live rays takes it
+  // (two forms in the waves whose rays disagree).
   auto soft_min_march = [&](const float p[3], bool fast, float Dprev, int& choice) {
     if constexpr (SPLIT) {
-      const bool far = !gone && !retired && !(psq(p) <= 1e10f);
-      const bool any_far = __ballot(far) != 0ull;
+      const bool live = !gone && !retired;
+      bool nr = live && shift_none_ok && 2.0f * fmaxf(Dprev, 0.0f) + a.lse_slack <= 90.0f * inv_kappa;
+      if (live && !nr && shift_none_ok && a.mfma)
+        nr = fixed_shift(p, kappa * kappa, Lds::v4(L.S0[0]), Lds::v4(L.S1[0])) - kr_first <= 90.0f;
+      const bool far = live && !nr && !(psq(p) <= 1e10f);
+      const bool use_fixed = !nr && shift_fixed_ok && !far;
+      const unsigned long long bn = __ballot(nr), bf = __ballot(live && use_fixed),
+                               bx = __ballot(live && !nr && !use_fixed);
       int cm = 0;
-      float Dm = 0.0f, Dx = 0.0f;
-      if (shift_fixed_ok) Dm = soft_min_core(p, fast, Dprev, cm, 1);
-      if (!shift_fixed_ok || any_far) Dx = soft_min_core(p, fast, Dprev, cm, 2);
-      const bool use_fixed = shift_fixed_ok && !far;
-      choice = (use_fixed ? 2 : 0) | (fast ? 4 : 0);
-      return use_fixed ? Dm : Dx;
+      float Dn = 0.0f, Dm = 0.0f, Dx = 0.0f;
+      if (bn != 0ull) Dn = soft_min_core(p, fast, Dprev, cm, 3);
+      if (bf != 0ull) Dm = soft_min_core(p, fast, Dprev, cm, 1);
+      if (bx != 0ull) Dx = soft_min_core(p, fast, Dprev, cm, 2);
+      choice = (nr ? 1 : 0) | (use_fixed ? 2 : 0) | (fast ? 4 : 0);
+      return nr ? Dn : (use_fixed ? Dm : Dx);
     } else {
       return soft_min_core(p, fast, Dprev, choice, 0);
     }
