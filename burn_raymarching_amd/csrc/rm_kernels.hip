@@ -2097,6 +2097,9 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       st0 = a.cont_resume;
     }
     const unsigned long long below = (1ull << lane) - 1ull;
+#ifdef RM_RAY_STATS  // measurement build: the march steps each ray needs (until gone or period 2)
+    int ray_need = st0;
+#endif
     for (int st = st0; !dead && st < a.steps; ++st) {
       if (SPLIT && a.cont_cap > 0 && st == a.cont_cap) {
         // ray mode, defer at the top of this step: every ray's state, the marching rays to the
@@ -2147,6 +2150,9 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       int choice;
       const float D = soft_min_march(p, all_safe(lb, rho_lb), Dprev, choice);
       const float t_step = t;  // this step's state: (t_step, choice)
+#ifdef RM_RAY_STATS
+      if (valid && !gone && !(t_step == cyc_t2 && choice == ((chist >> 3) & 7))) ray_need = st + 1;
+#endif
       if constexpr (SPLIT) {
         // Ray mode: a ray's step is a function of its own t (the shift is scene-uniform; the clamp
         // choice changes no bit), so a ray whose t repeats with period 2 (t_step == t two steps
@@ -2248,6 +2254,14 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
         chist = ((chist << 3) | choice) & 0xFFF;
       }
     }
+#ifdef RM_RAY_STATS
+    if (!SPLIT && a.stats != nullptr) {  // stats[3]: the needed lane-steps, summed
+      unsigned long long v = valid ? (unsigned long long)ray_need : 0ull;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+      if (lane == 0) atomicAdd(a.stats + 3, v);
+    }
+#endif
     if (SPLIT && a.ray_cont) {
       // ray mode: the listed rays' final states back into their groups' rows (the resume launch
       // runs the groups' post-march forward and backward); the steps this block ran uncounted
@@ -4816,6 +4830,10 @@ int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset) {
   out->seeded_rays_a = (int64_t)v[5];
 #ifdef RM_LANE_STATS
   std::fprintf(stderr, "RM_LANE_STATS escaped_lane_sweeps %llu\n", v[3]);
+#endif
+#ifdef RM_RAY_STATS
+  std::fprintf(stderr, "RM_RAY_STATS needed_lane_steps %llu waves %lld steps_saved %llu\n", v[3],
+               (long long)ctx->stats_waves, v[2]);
 #endif
   if (reset) {
     RM_HIP(ctx, hipMemsetAsync(ctx->stats_dev, 0, sizeof v, ctx->stream));
