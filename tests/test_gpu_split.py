@@ -278,3 +278,63 @@ def test_split_costs_no_accuracy(rm, oracle, monkeypatch, m):
         assert ea <= 1.5 * eb + 1e-6, key
         for e in (ea, eb):
             assert e <= grad_errors(g32[key], ref)[1], key
+
+
+@pytest.mark.parametrize("k,flag", [(5.0, None), (32.0, "FORCE_MAX_SHIFT"), (32.0, "VALU_ONLY")])
+def test_split_ray_mode_forms(rm, monkeypatch, k, flag):
+    """Ray mode under the other soft-min paths: at k = 5 (the reference loop's first stage: the
+    forms differ between rays more often), with the running maximum forced for every step
+    (RM_MARCH_FORCE_MAX_SHIFT) and on the vector-only march (RM_MARCH_VALU_ONLY). The default
+    continuation at S = 128 (five launches) equals one launch and the march with the exit off, bit
+    for bit."""
+    render, model, native = rm
+    W = H = 48
+    M, S = 300, 128
+    s = model.scene_tensors(model.synthetic_scene(M, 31, radius_range=(0.02, 0.08)))
+    cams = model.ring_cameras(10, offset=7)[:1]
+    tg = render.render_diff_camera(cams, W, H, model.scene_tensors(model.synthetic_scene(M, 32)), k, S)
+    f = getattr(native, "RM_MARCH_" + flag) if flag else 0
+    monkeypatch.setenv("RM_SPLIT", "1")
+    monkeypatch.delenv("RM_SPLIT_CONT_STEPS", raising=False)
+    monkeypatch.delenv("RM_SPLIT_CONT_LIST", raising=False)
+    ctx = render.context()
+    ctx.collect_timing(reset=True)
+    ctx.timing(True)
+    base = _train(render, native, cams, W, H, tg, s, k, S, flags=f)
+    ctx.timing(False)
+    assert ctx.collect_timing(reset=True)[1] == 5
+    _equal(base, _train(render, native, cams, W, H, tg, s, k, S, flags=f | native.RM_MARCH_NO_EARLY_EXIT))
+    monkeypatch.setenv("RM_SPLIT_CONT_STEPS", "0")
+    _equal(base, _train(render, native, cams, W, H, tg, s, k, S, flags=f))
+
+
+def test_split_ray_mode_array_ragged(rm, oracle, monkeypatch):
+    """Array-mode train steps continue at the caps like camera mode, with a ragged last block
+    (777 rays: 24 blocks of 32 and one of 9) and rays listed from any block: the same loss,
+    gradients and image as one launch, bit for bit."""
+    render, model, native = rm
+    M, S, K = 300, 128, 32.0
+    sc = model.synthetic_scene(M, 33, radius_range=(0.02, 0.08))
+    s = model.scene_tensors(sc)
+    cams = model.ring_cameras(10, offset=1)[:1]
+    o, d = cam_rays(oracle, cams, 48, 48)
+    sel = np.random.default_rng(5).permutation(o.shape[0])[:777]  # scattered rays: ragged, mixed tiles
+    o, d = o[sel], d[sel]
+    tg = np.random.default_rng(6).uniform(0.0, 1.0, size=o.shape).astype(np.float32)
+    monkeypatch.setenv("RM_SPLIT", "1")
+    monkeypatch.delenv("RM_SPLIT_CONT_LIST", raising=False)
+    got = []
+    for env in (None, "0"):
+        if env is None:
+            monkeypatch.delenv("RM_SPLIT_CONT_STEPS", raising=False)
+        else:
+            monkeypatch.setenv("RM_SPLIT_CONT_STEPS", env)
+        ctx = render.context()
+        ctx.collect_timing(reset=True)
+        ctx.timing(True)
+        loss, g, out = render.train_step(dev(o), dev(d), dev(tg), s, K, 0.3, S, with_out=True)
+        ctx.timing(False)
+        got.append((host(loss), {key: host(v) for key, v in g.items()}, host(out),
+                    ctx.collect_timing(reset=True)[1]))
+    assert got[0][3] == 5 and got[1][3] == 1
+    _equal(got[0][:3], got[1][:3])
