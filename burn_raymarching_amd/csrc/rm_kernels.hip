@@ -1956,6 +1956,10 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
       if (bn != 0ull) Dn = soft_min_core(p, fast, Dprev, cm, 3);
       if (bf != 0ull) Dm = soft_min_core(p, fast, Dprev, cm, 1);
       if (bx != 0ull) Dx = soft_min_core(p, fast, Dprev, cm, 2);
+      // exit off (the capability measurement: every ray does every step's work): a wave whose
+      // rays are all gone still runs a sweep, as the wave-uniform march does (results unused)
+      if (!a.early_exit && (bn | bf | bx) == 0ull)
+        Dn = soft_min_core(p, fast, Dprev, cm, shift_none_ok ? 3 : (shift_fixed_ok ? 1 : 2));
       choice = (nr ? 1 : 0) | (use_fixed ? 2 : 0) | (fast ? 4 : 0);
       return nr ? Dn : (use_fixed ? Dm : Dx);
     } else {
