@@ -1949,17 +1949,16 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
         nr = fixed_shift(p, kappa * kappa, Lds::v4(L.S0[0]), Lds::v4(L.S1[0])) - kr_first <= 90.0f;
       const bool far = live && !nr && !(psq(p) <= 1e10f);
       const bool use_fixed = !nr && shift_fixed_ok && !far;
-      const unsigned long long bn = __ballot(nr), bf = __ballot(live && use_fixed),
-                               bx = __ballot(live && !nr && !use_fixed);
+      unsigned long long bn = __ballot(nr);
+      const unsigned long long bf = __ballot(live && use_fixed), bx = __ballot(live && !nr && !use_fixed);
+      // exit off (the capability measurement: every ray does every step's work): a wave whose
+      // rays are all gone still runs a sweep, as the wave-uniform march does (results unused)
+      if (!a.early_exit && (bn | bf | bx) == 0ull) bn = 1ull;
       int cm = 0;
       float Dn = 0.0f, Dm = 0.0f, Dx = 0.0f;
       if (bn != 0ull) Dn = soft_min_core(p, fast, Dprev, cm, 3);
       if (bf != 0ull) Dm = soft_min_core(p, fast, Dprev, cm, 1);
       if (bx != 0ull) Dx = soft_min_core(p, fast, Dprev, cm, 2);
-      // exit off (the capability measurement: every ray does every step's work): a wave whose
-      // rays are all gone still runs a sweep, as the wave-uniform march does (results unused)
-      if (!a.early_exit && (bn | bf | bx) == 0ull)
-        Dn = soft_min_core(p, fast, Dprev, cm, shift_none_ok ? 3 : (shift_fixed_ok ? 1 : 2));
       choice = (nr ? 1 : 0) | (use_fixed ? 2 : 0) | (fast ? 4 : 0);
       return nr ? Dn : (use_fixed ? Dm : Dx);
     } else {
