@@ -292,7 +292,14 @@ __host__ __device__ inline size_t tiles_offset(int npairs, int nprep) {
 }
 // Then the escape thresholds of the march: kEscTab floats (see write_bound).
 constexpr int kEscTab = 64;
+#ifdef RM_RAY_STATS
+constexpr int kStatsWords = 8;  // + [6] / [7]: lane-steps after the cap, run and compacted (measurement)
+#ifndef RM_RAY_STATS_CAP
+#define RM_RAY_STATS_CAP 16
+#endif
+#else
 constexpr int kStatsWords = 6;  // rm_stats device counters (KArgs::stats)
+#endif
 [[maybe_unused]] constexpr int kDeadCountSlot = 44;  // Lds::misc int: the hand-off's count of waves that ended early
 __host__ __device__ inline size_t esc_offset(int npairs, int nprep) {
   const size_t nrb = (size_t)npairs / 8;
@@ -1649,6 +1656,9 @@ __global__ __launch_bounds__(kBlock, RM_CONT_MIN_WAVES) void rm_cont_kernel(cons
 template <int MODE, bool CAM, bool SPLIT>
 __device__ __forceinline__ void ray_body(const KArgs& a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+#ifdef RM_RAY_STATS
+  __shared__ unsigned rs_w[3];  // measurement build (see the march)
+#endif
   Lds L;
   {
     const int np = a.Mpad / 2;
@@ -2102,6 +2112,12 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
     const unsigned long long below = (1ull << lane) - 1ull;
 #ifdef RM_RAY_STATS  // measurement build: the march steps each ray needs (until gone or period 2)
     int ray_need = st0;
+    // and what packing a block's rays still marching at step RM_RAY_STATS_CAP into the fewest
+    // waves would leave of its waves' steps after it (unsplit): live rays, summed steps, max steps
+    if (tid < 3) rs_w[tid] = 0u;
+    __syncthreads();
+    bool rs_at = false;
+    int rs_last = st0 - 1;
 #endif
     for (int st = st0; !dead && st < a.steps; ++st) {
       if (SPLIT && a.cont_cap > 0 && st == a.cont_cap) {
@@ -2150,6 +2166,14 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
         st_stop = st;
         break;
       }
+#ifdef RM_RAY_STATS
+      if (!SPLIT && st == RM_RAY_STATS_CAP) {
+        const int lv = __popcll(__ballot(valid && !gone && ray_need >= st));
+        if (lane == 0) atomicAdd(&rs_w[0], (unsigned)lv);
+        rs_at = true;
+      }
+      rs_last = st;
+#endif
       int choice;
       const float D = soft_min_march(p, all_safe(lb, rho_lb), Dprev, choice);
       const float t_step = t;  // this step's state: (t_step, choice)
@@ -2263,6 +2287,10 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
 #pragma unroll
       for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
       if (lane == 0) atomicAdd(a.stats + 3, v);
+      if (rs_at && lane == 0) {
+        atomicAdd(&rs_w[1], (unsigned)(rs_last + 1 - RM_RAY_STATS_CAP));
+        atomicMax(&rs_w[2], (unsigned)(rs_last + 1 - RM_RAY_STATS_CAP));
+      }
     }
 #endif
     if (SPLIT && a.ray_cont) {
@@ -2554,6 +2582,12 @@ __device__ __forceinline__ void ray_body(const KArgs& a) {
   }
 #endif
   __syncthreads();
+#ifdef RM_RAY_STATS
+  if (!SPLIT && tid == 0 && a.stats != nullptr && rs_w[1] != 0u) {
+    atomicAdd(a.stats + 6, 64ull * rs_w[1]);
+    atomicAdd(a.stats + 7, 64ull * ((rs_w[0] + 63u) / 64u) * rs_w[2]);
+  }
+#endif
   int alive = 0;
 #pragma unroll
   for (int w = 0; w < (SPLIT ? kSplitWaves : kWaves); ++w) alive |= wflag[w] ? 0 : (1 << w);
@@ -4835,8 +4869,8 @@ int rm_stats_collect(rm_context* ctx, rm_stats* out, int32_t reset) {
   std::fprintf(stderr, "RM_LANE_STATS escaped_lane_sweeps %llu\n", v[3]);
 #endif
 #ifdef RM_RAY_STATS
-  std::fprintf(stderr, "RM_RAY_STATS needed_lane_steps %llu waves %lld steps_saved %llu\n", v[3],
-               (long long)ctx->stats_waves, v[2]);
+  std::fprintf(stderr, "RM_RAY_STATS needed_lane_steps %llu waves %lld steps_saved %llu after_cap_run %llu "
+               "after_cap_packed %llu\n", v[3], (long long)ctx->stats_waves, v[2], v[6], v[7]);
 #endif
   if (reset) {
     RM_HIP(ctx, hipMemsetAsync(ctx->stats_dev, 0, sizeof v, ctx->stream));
