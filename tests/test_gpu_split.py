@@ -338,3 +338,33 @@ def test_split_ray_mode_array_ragged(rm, oracle, monkeypatch):
                     ctx.collect_timing(reset=True)[1]))
     assert got[0][3] == 5 and got[1][3] == 1
     _equal(got[0][:3], got[1][:3])
+
+
+def test_split_ray_mode_sub_launches(rm, oracle, monkeypatch):
+    """A call split into sub-launches (RM_MAX_BLOCKS_PER_LAUNCH=40: 90 groups of 32 rays in three
+    sub-launches, gradients accumulated) continues each sub-launch at the caps with the buffers of
+    the one before reused: the same bits as one launch per sub-launch, and within the oracle's
+    tolerance of the whole-call result."""
+    render, model, native = rm
+    M, S, K = 300, 128, 32.0
+    sc = model.synthetic_scene(M, 35, radius_range=(0.02, 0.08))
+    s = model.scene_tensors(sc)
+    cams = model.ring_cameras(10, offset=8)[:3]
+    tg = render.render_diff_camera(cams, 40, 24, model.scene_tensors(model.synthetic_scene(M, 36)), K, S)
+    monkeypatch.setenv("RM_SPLIT", "1")
+    monkeypatch.delenv("RM_SPLIT_CONT_LIST", raising=False)
+    monkeypatch.delenv("RM_SPLIT_CONT_STEPS", raising=False)
+    whole = _train(render, native, cams, 40, 24, tg, s, K, S)
+    monkeypatch.setenv("RM_MAX_BLOCKS_PER_LAUNCH", "40")
+    ctx = render.context()
+    ctx.collect_timing(reset=True)
+    ctx.timing(True)
+    sub = _train(render, native, cams, 40, 24, tg, s, K, S)
+    ctx.timing(False)
+    assert ctx.collect_timing(reset=True)[1] == 3 * 5
+    monkeypatch.setenv("RM_SPLIT_CONT_STEPS", "0")
+    _equal(sub, _train(render, native, cams, 40, 24, tg, s, K, S))
+    np.testing.assert_array_equal(sub[2], whole[2])  # the image does not depend on the grouping
+    for key in KEYS:
+        a, b = sub[1][key], whole[1][key]
+        assert np.abs(a - b).max() <= 1e-5 * max(np.abs(b).max(), 1e-12), key
