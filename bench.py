@@ -261,6 +261,16 @@ def load_target_files(cameras_json, entries, W, H):
     return np.stack(out)
 
 
+def _json_stdout():
+    """The stream for the one JSON line: the process's stdout, while fd 1 itself points at stderr
+    for the rest of the run, so that what libraries write there (gloo's connection banner, HIP or
+    RCCL diagnostics) cannot interleave the line the driver parses."""
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    return os.fdopen(fd, "w", buffering=1)
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -275,6 +285,7 @@ def main():
         print(json.dumps({"rank": rank, "local_rank": local, "world": world,
                           "master": f"{os.environ.get('MASTER_ADDR')}:{os.environ.get('MASTER_PORT')}"}), flush=True)
         return
+    json_out = _json_stdout()
 
     import torch
     # RM_BENCH_BACKEND=gloo: rehearsal of the N-rank path on fewer GPUs than ranks (ranks share
@@ -760,7 +771,8 @@ def main():
                            "march_steps_saved_frac": round(march_saved_frac, 4)},
             "finite": finite,
         }
-        print(json.dumps(line), flush=True)
+        json_out.write(json.dumps(line) + "\n")
+        json_out.flush()
         if args.dump_grad and grad0:
             np.save(args.dump_grad, grad0[0].cpu().numpy())
     if dist is not None:
