@@ -368,3 +368,25 @@ def test_split_ray_mode_sub_launches(rm, oracle, monkeypatch):
     for key in KEYS:
         a, b = sub[1][key], whole[1][key]
         assert np.abs(a - b).max() <= 1e-5 * max(np.abs(b).max(), 1e-12), key
+
+
+def test_split_ray_mode_saved_t(rm, oracle, monkeypatch):
+    """The split backward from the forward's saved march t (t_march: no march, no continuation)
+    equals the backward that marches again through the ray-mode continuations, bit for bit; the
+    forward's t is the same whether its march ran in one launch or not (forward calls never
+    continue), and retired and gone rays hand over their final t."""
+    render, model, _ = rm
+    M, S, K = 300, 128, 32.0
+    sc = model.synthetic_scene(M, 37, radius_range=(0.02, 0.08))
+    s = model.scene_tensors(sc)
+    cams = model.ring_cameras(10, offset=9)[:1]
+    o, d = cam_rays(oracle, cams, 48, 48)
+    monkeypatch.setenv("RM_SPLIT", "1")
+    monkeypatch.delenv("RM_SPLIT_CONT_LIST", raising=False)
+    monkeypatch.delenv("RM_SPLIT_CONT_STEPS", raising=False)
+    _, t = render.render_diff_forward(dev(o), dev(d), s, K, S, return_t=True)
+    g = dev(np.random.default_rng(8).normal(size=o.shape).astype(np.float32))
+    a = render.render_diff_backward(dev(o), dev(d), s, K, g, S)
+    b = render.render_diff_backward(dev(o), dev(d), s, K, g, S, t_march=t)
+    for key in a:
+        assert np.array_equal(host(a[key]), host(b[key])), key
